@@ -1,0 +1,228 @@
+/*
+ * marlsc.h -- C ABI of the MI355X-native vectorised supply-chain environment (libmarlsc.so).
+ *
+ * Drop-in boundary for the reference's env hot path. One `msc_env` handle owns E independent
+ * copies of the reference's `InventoryEnvironment` (src/environment/envs/multi_env.py:38)
+ * resident in HBM and steps them in lockstep on one GPU. Entry points and the reference
+ * interface each one replaces:
+ *
+ *   msc_env_create   <- InventoryEnvironment.__init__(env_config, seed, env_meta)   multi_env.py:58-190
+ *                       + per-env seeds of the RLlib env factory
+ *                         SeedManager.derive_env_seed(base, worker_index, env_index)  seed_manager.py:165-186
+ *                         (called from src/algorithms/base.py:413-419)
+ *   msc_env_reset    <- InventoryEnvironment.reset(seed=None, options=None)          multi_env.py:192-251
+ *                       (SeedManager.advance_episode / update_root_seed, seed_manager.py:100-136)
+ *   msc_env_step     <- InventoryEnvironment.step(actions)                            multi_env.py:253-366
+ *                       (the five components: demand_sampler.py:105-163 / :214-261,
+ *                        demand_allocator.py:118-217, lead_time_sampler.py:97-108 / :169-197,
+ *                        lost_sales_handler.py:71-210, reward_calculator.py:96-190)
+ *                       plus RLlib's reset-after-truncation of the EnvRunner loop.
+ *   msc_env_obs_flat <- the flat per-agent observation  local_i || concat_j local_j   multi_env.py:548-575
+ *   msc_gae          <- RLlib 2.52.1 GAE + advantage standardisation (external to the reference;
+ *                       enabled at src/algorithms/mappo.py:154-156)
+ *
+ * Conventions
+ *   - Return value 0 = OK, negative = error; msc_last_error() gives a thread-local message.
+ *   - All array arguments of msc_env_step / msc_env_reset / msc_gae are DEVICE pointers
+ *     (e.g. torch data_ptr()) unless the parameter name ends in `_host`.
+ *   - Every call is stream-ordered on the given hipStream_t (pass 0 for the null stream); no call
+ *     synchronises the device except msc_env_create / msc_env_destroy / msc_env_read_state /
+ *     msc_env_write_state / msc_env_check.
+ *   - The library owns the env state buffers; callers own every I/O buffer.
+ *   - One handle per stream / host thread; a handle is not thread-safe (like the reference object).
+ *   - Layouts are row-major: actions [E][W][K] f32, obs [E][W][L] f32, rewards [E][W].
+ */
+#ifndef MARLSC_H
+#define MARLSC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct msc_env msc_env;
+typedef struct ihipStream_t* msc_stream_t; /* == hipStream_t */
+
+#define MSC_ABI_VERSION 1
+#define MSC_MAX_W 16   /* warehouses (agents) per env */
+#define MSC_MAX_K 8    /* SKUs */
+#define MSC_MAX_R 4096 /* demand regions */
+#define MSC_HISTORY 5  /* rolling window, multi_env.py:147 */
+
+/* Component `type` strings of the reference's registries (src/environment/registry.py:300-308). */
+enum msc_demand_type   { MSC_DEMAND_POISSON = 0, MSC_DEMAND_EMPIRICAL = 1 };
+enum msc_action_type   { MSC_ACTION_DIRECT = 0, MSC_ACTION_DEMAND_CENTERED = 1, MSC_ACTION_BASE_STOCK = 2 };
+enum msc_init_type     { MSC_INIT_UNIFORM = 0, MSC_INIT_CUSTOM = 1, MSC_INIT_ZERO = 2 };
+enum msc_lead_type     { MSC_LEAD_FIXED = 0, MSC_LEAD_STOCHASTIC = 1 };
+enum msc_lost_type     { MSC_LOST_CLOSEST = 0, MSC_LOST_SHIPMENT = 1, MSC_LOST_COST = 2 };
+enum msc_scope         { MSC_SCOPE_AGENT = 0, MSC_SCOPE_TEAM = 1 };
+enum msc_obs_norm      { MSC_OBS_OFF = 0, MSC_OBS_RATIO = 1, MSC_OBS_MEANSTD = 2 };
+
+/* Feature toggles (FeatureConfig, src/config/schema.py:595-639); order = block order of
+ * _build_local_obs (multi_env.py:620-695). */
+enum msc_feature_bits {
+  MSC_F_INVENTORY = 1u << 0,            MSC_F_INVENTORY_AGG = 1u << 1,
+  MSC_F_PIPELINE = 1u << 2,             MSC_F_PIPELINE_AGG = 1u << 3,
+  MSC_F_INCOMING_HOME = 1u << 4,        MSC_F_INCOMING_HOME_AGG = 1u << 5,
+  MSC_F_SHIPPED_HOME = 1u << 6,
+  MSC_F_SHIPPED_AWAY = 1u << 7,         MSC_F_SHIPPED_AWAY_AGG = 1u << 8,
+  MSC_F_STOCKOUT = 1u << 9,
+  MSC_F_ROLLING_MEAN = 1u << 10,        MSC_F_ROLLING_MEAN_AGG = 1u << 11,
+  MSC_F_FORECAST = 1u << 12,            MSC_F_FORECAST_AGG = 1u << 13,
+  MSC_F_DAYS_OF_SUPPLY = 1u << 14,
+  MSC_F_NET_POSITION = 1u << 15,
+  MSC_F_DEMAND_VARIABILITY = 1u << 16,
+  MSC_F_DEMAND_HISTORY = 1u << 17
+};
+
+/* Environment descriptor: the reference's EnvironmentConfig + env_meta flattened to plain
+ * host arrays (all HOST pointers; copied by msc_env_create). Shapes use W = n_warehouses,
+ * K = n_skus, R = n_regions. */
+typedef struct msc_env_desc {
+  int32_t abi_version;                 /* = MSC_ABI_VERSION */
+  int32_t n_warehouses, n_skus, n_regions, episode_length;
+
+  int32_t action_type;                 /* msc_action_type */
+  const double* action_param;          /* [K]: max_order_quantities | max_quantity_adjustment | max_stock_level */
+
+  int32_t init_type;                   /* msc_init_type */
+  int32_t init_min, init_max;          /* uniform: integers(min, max+1, (W,K)) (multi_env.py:522-525) */
+  const int32_t* init_values;          /* custom: [W*K] */
+
+  int32_t holding_per_sku;             /* 1: holding_cost is [K]; 0: scalar x sku_weights */
+  const double* holding_cost;
+  int32_t penalty_per_sku;
+  const double* penalty_cost;
+  const double* sku_weights;           /* [K] */
+  const double* distances;             /* [W*R] */
+  const double* outbound_fixed;        /* [W*R] */
+  const double* outbound_variable;     /* [W*R] */
+  const double* inbound_fixed;         /* [W*K] */
+  const double* inbound_variable;      /* [W*K] */
+
+  int32_t demand_type;                 /* msc_demand_type */
+  const double* lambda_orders;         /* poisson: [R] (scalar mode: broadcast by the caller) */
+  const double* probability_skus;      /* [R] */
+  const double* lambda_quantity;       /* [R*K] */
+  /* empirical trace, CSR over the sorted available timesteps (demand_sampler.py:199-261):
+   * orders of trace row i are [trace_offsets[i], trace_offsets[i+1]), each with a region and
+   * K quantities, already grouped/sorted by (region_id, order_id). */
+  int32_t trace_n_rows;
+  const int64_t* trace_offsets;        /* [trace_n_rows + 1] */
+  const int32_t* trace_regions;        /* [n_trace_orders] */
+  const int32_t* trace_quantities;     /* [n_trace_orders * K] */
+
+  int32_t max_splits;                  /* greedy allocator ("default" -> W-1) */
+
+  int32_t lead_type;                   /* msc_lead_type */
+  const int32_t* expected_lead_times;  /* [W*K] */
+  int32_t max_dev_per_sku;             /* 1: max_deviation is [K] (SKU-major draws); 0: scalar */
+  const int32_t* max_deviation;
+
+  int32_t lost_type;                   /* msc_lost_type */
+  double lost_alpha;                   /* softmax temperature for MSC_LOST_COST */
+
+  int32_t reward_scope;                /* msc_scope */
+  double reward_scale;
+
+  uint32_t feature_flags;              /* msc_feature_bits */
+  int32_t include_warehouse_id;        /* one-hot prefix (parameter sharing) */
+  int32_t obs_norm;                    /* msc_obs_norm */
+  const float* obs_mean;               /* [n_features] for MSC_OBS_MEANSTD */
+  const float* obs_std;
+  int32_t num_eval_episodes;           /* <= 0: no eval cycling (multi_env.py:164-168, 220-224) */
+} msc_env_desc;
+
+/* Optional per-step diagnostics = the reference's collect_step_info dict (multi_env.py:330-361).
+ * DEVICE pointers, any may be NULL. */
+typedef struct msc_step_info {
+  int32_t* inventory_before;           /* [E][W][K] */
+  int32_t* pending_total;              /* [E][W][K] */
+  int32_t* order_quantities;           /* [E][W][K] */
+  int32_t* demand_per_region;          /* [E][R][K] */
+  int32_t* fulfilled_per_warehouse;    /* [E][W][K] */
+  int32_t* unfulfilled_demands;        /* [E][R][K] */
+  int32_t* shipment_counts;            /* [E][W][R] */
+  int32_t* shipment_quantities;        /* [E][W][R] */
+  int32_t* shipment_quantities_by_sku; /* [E][W][R][K] */
+  int32_t* lost_order_counts;          /* [E][R] */
+  int32_t* n_orders;                   /* [E] */
+  double* lost_sales;                  /* [E][W][K] */
+  double* costs;                       /* [E][4][W]: holding, penalty, outbound, inbound */
+} msc_step_info;
+
+/* Create E = n_envs environments on `device`. Env i gets root seed
+ *   env_seeds_host[i]                                    if env_seeds_host != NULL, else
+ *   SeedSequence([base_seed, worker_index, env_index_offset + i]).generate_state(1)[0].
+ * Nothing is reset yet: call msc_env_reset before the first step. */
+int msc_env_create(const msc_env_desc* desc, int device, int64_t n_envs, uint32_t base_seed,
+                   uint32_t worker_index, int64_t env_index_offset, const uint32_t* env_seeds_host,
+                   msc_env** out);
+void msc_env_destroy(msc_env* env);
+
+/* Sizes of the I/O tensors. */
+int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t* n_skus,
+                 int32_t* n_regions, int32_t* local_obs_dim, int32_t* n_features,
+                 int32_t* max_expected_lead_time);
+
+#define MSC_RESET_EVAL_RESTART 1  /* reset(seed=...) of a construction-seeded eval env: counter -> 0 */
+
+/* Reset envs with mask[i] != 0 (mask == NULL: all). new_root_seeds == NULL follows the
+ * construction-seeded path (advance_episode, with eval cycling); otherwise
+ * update_root_seed(new_root_seeds[i]) (reset(seed=X) of an env created without a seed).
+ * Writes the reset observation of every reset env into obs [E][W][L] (may be NULL). */
+int msc_env_reset(msc_env* env, const uint8_t* mask, const uint32_t* new_root_seeds, int32_t flags,
+                  float* obs, msc_stream_t stream);
+
+/* One step of every env. actions [E][W][K] in [-1, 1]. Outputs obs [E][W][L] (local obs of
+ * every agent), rewards [E][W] (f32, and optionally f64), truncated [E]. An env whose episode
+ * ends is reset in the same call (RLlib's EnvRunner semantics): its terminal observation goes
+ * to final_obs (if non-NULL) and obs receives the first observation of the next episode. */
+int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
+                 double* rewards_f64, uint8_t* truncated, float* final_obs,
+                 const msc_step_info* info, msc_stream_t stream);
+
+/* Flat per-agent observation of the reference [E][W][L*(1+W)] = local_w || local_0..local_{W-1},
+ * from the compact obs [E][W][L]. */
+int msc_env_obs_flat(const msc_env* env, const float* obs, float* flat, msc_stream_t stream);
+
+/* Host copies of the parity-relevant state (synchronous). Any pointer may be NULL.
+ *   inventory [E][W][K] i32, timestep [E], episode_counter [E],
+ *   rng [E][2][6] u64: {demand, lead_time} x {state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger} */
+int msc_env_read_state(const msc_env* env, int32_t* inventory_host, int32_t* timestep_host,
+                       int32_t* episode_counter_host, uint64_t* rng_host);
+
+/* Opaque checkpoint of the whole device state (synchronous): size query, save, restore. */
+int64_t msc_env_state_bytes(const msc_env* env);
+int msc_env_save_state(const msc_env* env, void* buf_host);
+int msc_env_load_state(msc_env* env, const void* buf_host);
+
+/* Synchronise and report device-side errors (order-buffer overflow, ...). */
+int msc_env_check(msc_env* env);
+
+/* Advantage estimation over T steps x N sequences (layout [T][N], time-major):
+ *   delta_t = r_t + gamma * V_{t+1} * (1 - term_t) - V_t
+ *   A_t     = delta_t + gamma * lam * (1 - term_t) * (1 - trunc_t) * A_{t+1}
+ * where V_{t+1} = next_values[t] if trunc_t (bootstrap from the terminal obs) else values[t+1];
+ * values[T] (row T of `values`, [T+1][N]) bootstraps the last row. targets = A + V.
+ * stats_out (device f64[3]) receives {sum A, sum A^2, count} (accumulated, caller zeroes it)
+ * for the cross-rank advantage standardisation. */
+int msc_gae(const float* rewards, const float* values, const float* next_values,
+            const uint8_t* terminated, const uint8_t* truncated, int64_t n_seq, int32_t T,
+            float gamma, float lam, float* advantages, float* targets, double* stats_out,
+            msc_stream_t stream);
+
+/* In-place (A - mean) / max(1e-4, std) using stats {sum, sumsq, count} (device f64[3]). */
+int msc_adv_normalize(float* advantages, int64_t n, const double* stats, msc_stream_t stream);
+
+/* Utility: SeedSequence(words).generate_state(1, uint32)[0] (numpy-compatible), on the host. */
+uint32_t msc_seedseq_u32(const uint32_t* words, int32_t n_words);
+
+const char* msc_last_error(void);
+int msc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MARLSC_H */

@@ -1,0 +1,61 @@
+"""Empirical demand trace -> CSR device layout (the input side of `EmpiricalDemandSampler`).
+
+The reference samples empirical demand from the preprocessor's output frame
+(src/data/preprocessor.py:682-696: columns timestep, region_id, order_id, sku_id, quantity) by
+filtering one timestep per call and grouping by (region_id, order_id) with pandas
+(src/environment/components/demand_sampler.py:199-261), ~42 ms per step at 256 regions.
+Here the frame is packed ONCE into CSR over the sorted available timesteps:
+
+    offsets[i] .. offsets[i+1]  = orders of the i-th available timestep, in groupby order
+    regions[j], quantities[j, :K] = region and per-SKU summed quantity of order j
+
+so that one env step reads its orders as a contiguous slice. SKU ids outside [0, K) are dropped
+like the reference (demand_sampler.py:255).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict
+
+import numpy as np
+
+
+def _frame_columns(src: Any):
+    cols = {}
+    for c in ("timestep", "region_id", "order_id", "sku_id", "quantity"):
+        cols[c] = np.asarray(src[c])
+    return cols
+
+
+def pack_demand_trace(src: Any, n_skus: int, data_mode: str = "train") -> Dict[str, Any]:
+    """src: DataFrame / dict of columns, or {"train": ..., "val": ...} (data_mode selects, as
+    `context.data_mode == "val"` does at demand_sampler.py:188-192)."""
+    if isinstance(src, dict) and "train" in src:
+        src = src["val"] if data_mode == "val" and src.get("val") is not None else src["train"]
+    c = _frame_columns(src)
+    ts_unique = np.unique(c["timestep"])
+    q = c["quantity"]
+    if np.any(q != np.round(q)) or np.any(q < 0) or np.any(q > 65535):
+        raise ValueError("trace quantities must be integers in [0, 65535]")
+    # group key order: timestep, region_id, order_id (lexicographic on the order id's own type)
+    oid = c["order_id"]
+    oid_codes = np.unique(oid, return_inverse=True)[1]
+    order = np.lexsort((oid_codes, c["region_id"], c["timestep"]))
+    ts, reg, oc = c["timestep"][order], c["region_id"][order].astype(np.int64), oid_codes[order]
+    sku, qty = c["sku_id"][order].astype(np.int64), q[order].astype(np.int64)
+    new = np.ones(len(ts), dtype=bool)
+    new[1:] = (ts[1:] != ts[:-1]) | (reg[1:] != reg[:-1]) | (oc[1:] != oc[:-1])
+    gid = np.cumsum(new) - 1
+    n_orders = int(gid[-1] + 1) if len(gid) else 0
+    quant = np.zeros((n_orders, n_skus), dtype=np.int64)
+    ok = (sku >= 0) & (sku < n_skus)
+    np.add.at(quant, (gid[ok], sku[ok]), qty[ok])
+    regions = reg[new].astype(np.int32)
+    order_ts = ts[new]
+    row = np.searchsorted(ts_unique, order_ts)
+    offsets = np.zeros(len(ts_unique) + 1, dtype=np.int64)
+    np.add.at(offsets, row + 1, 1)
+    offsets = np.cumsum(offsets)
+    if np.any(quant > 65535):
+        raise ValueError("summed order quantity exceeds 65535")
+    return {"n_rows": int(len(ts_unique)), "timesteps": ts_unique, "offsets": offsets,
+            "regions": regions, "quantities": quant.astype(np.int32)}
