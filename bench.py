@@ -1,0 +1,201 @@
+#!/usr/bin/env python
+"""Benchmark of the env hot path: `InventoryEnvironment.step()` of Jakoebly/marl-sc
+(src/environment/envs/multi_env.py:253-366) on MI355X through libmarlsc.
+
+A "step" = one pass of msc_env_step over every env of the rank (demand generation kernel +
+fused step kernel, including in-kernel auto-resets every episode_length steps), with synthetic
+uniform[-1, 1] actions already resident in HBM. Metric: agent-steps/s = envs x agents x steps / s,
+whole job. N > 1: one process per GPU (torchrun), each rank owns `--envs` envs with disjoint global
+env ids (weak scaling, no data-path collective); barrier + synchronize bracket the timed region
+and the max over ranks is reported.
+
+Roofline: average device duration of each kernel measured with HIP events on the launch stream
+(torch's current stream); algorithmic bytes per launch from the state layout.
+cpu_baseline: the C oracle (oracle/, a scalar port of the reference) timed on the host cores on a
+bounded sample of the same workload, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "marl-sc_amd"))
+sys.path.insert(0, str(REPO / "oracle"))
+
+BASELINE = json.loads((REPO / "BASELINE.json").read_text())
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+
+
+def ensure_built():
+    lib = REPO / "marl-sc_amd" / "marlsc" / "_lib" / "libmarlsc.so"
+    if not lib.exists():
+        subprocess.run(["make", "-s", "-C", str(REPO / "marl-sc_amd"), "-j8"], check=True)
+
+
+def algorithmic_bytes(spec, mean_orders: float):
+    """Minimum HBM bytes one env moves per step (see DESIGN.md section 'Roofline')."""
+    W, K, L = spec.W, spec.K, spec.local_obs_dim
+    WK = W * K
+    ring = max(int(spec.expected_lead_times.max()) + (int(spec.max_deviation.max()) if spec.lead_type == "stochastic" else 0) + 1, 2)
+    nv = (1 + K + 7) // 8
+    rec = 16 * nv
+    demand = 32 + 32 + 4 + rec * mean_orders  # rng state in/out, count, order records out
+    step = (2 * WK * 4            # inventory r/w
+            + WK * ring * 4       # pending ring read
+            + 2 * WK * 4          # new order + arrival clear
+            + WK * 4 + 4 * WK * 4  # history: new entry + 4 older entries for the rolling mean
+            + 2 * WK * 4          # incoming home demand r/w
+            + 2 * WK * 4          # EMA forecast r/w
+            + rec * mean_orders   # order records in
+            + WK * 4              # actions
+            + W * L * 4           # local observations
+            + W * 4 + 1 + 8)      # rewards, truncation, timestep
+    return demand, step
+
+
+def cpu_baseline(spec, seconds: float):
+    import numpy as np
+    import oracle as orc
+    threads = max(1, min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    E = 32 * threads
+    env = orc.OracleEnv(spec, E, base_seed=4321)
+    env.reset()
+    rng = np.random.default_rng(0)
+    acts = [rng.uniform(-1, 1, (E, spec.W, spec.K)).astype(np.float32) for _ in range(4)]
+    t0 = time.perf_counter()
+    env.step(acts[0], n_threads=threads)
+    one = time.perf_counter() - t0
+    steps = int(max(3, min(2000, seconds / max(one, 1e-6))))
+    t0 = time.perf_counter()
+    for i in range(steps):
+        env.step(acts[i % 4], n_threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/msc_oracle.c (scalar C port of the reference step), {E} envs x {steps} steps of "
+                      f"the same {spec.W}x{spec.R}x{spec.K} workload, OpenMP over envs, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=32768, help="envs per GPU")
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--regions", type=int, default=64)
+    ap.add_argument("--skus", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    if rank == 0:
+        ensure_built()
+    if world > 1:
+        dist.barrier()
+
+    from marlsc import make_synthetic_env_config
+    from marlsc.seeding import default_train_seed
+    from marlsc.spec import EnvSpec
+    from marlsc.vec_env import VecInventoryEnv
+
+    cfg = make_synthetic_env_config(args.agents, args.regions, args.skus)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    E = args.envs
+    dev = torch.cuda.current_device()
+    env = VecInventoryEnv(None, E, spec=spec, device=dev, base_seed=default_train_seed(42), env_index_offset=rank * E)
+    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    pool = [torch.rand((E, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
+    env.reset()
+    for i in range(args.warmup):
+        env.step(pool[i % 8])
+    env.check()
+
+    K = args.steps
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        e0, e1, e2 = evs[i]
+        e0.record()
+        env.generate_demand()
+        e1.record()
+        env.step(pool[i % 8])
+        e2.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    env.check()
+    t_demand = sum(a.elapsed_time(b) for a, b, _ in evs) / K / 1e3
+    t_step = sum(b.elapsed_time(c) for _, b, c in evs) / K / 1e3
+    tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+
+    if rank == 0:
+        value = E * world * spec.W * K / dt
+        mean_orders = float(spec.lambda_orders.sum())
+        b_dem, b_step = algorithmic_bytes(spec, mean_orders)
+        kern = {"demand_poisson_kernel": (t_demand, b_dem * E), "step_kernel": (t_step, b_step * E)}
+        dom = max(kern, key=lambda k: kern[k][0])
+        t_dom, bytes_dom = kern[dom]
+        traffic = None
+        tj = Path(args.traffic_json)
+        if tj.exists():
+            tr = json.loads(tj.read_text())
+            key = f"{spec.W}x{spec.R}x{spec.K}x{E}"
+            traffic = tr.get(key, {}).get(dom)
+        achieved = bytes_dom / t_dom / 1e9
+        out = {
+            "metric": BASELINE["metric"],
+            "value": round(value, 1),
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32 state, u64 PCG64, f64 rewards, f32 obs",
+            "data": "synthetic (SURVEY.md 8(d) cost structure, Poisson demand lambda_o=4 p=0.667 lambda_q=5, uniform[-1,1] actions)",
+            "config": {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x "
+                                   f"{spec.K} SKUs (BASELINE configs[2]; configs[3] when N>1)",
+                       "n_envs_per_gpu": E, "agents": spec.W, "regions": spec.R, "skus": spec.K,
+                       "episode_length": spec.episode_length, "obs_dim_local": spec.local_obs_dim,
+                       "parallelism": f"env-shard x{world}"},
+            "kernels_ms": {"demand_poisson_kernel": round(t_demand * 1e3, 4), "step_kernel": round(t_step * 1e3, 4)},
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic, "bytes_per_launch": int(bytes_dom)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

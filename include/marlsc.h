@@ -183,6 +183,12 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
                  double* rewards_f64, uint8_t* truncated, float* final_obs,
                  const msc_step_info* info, msc_stream_t stream);
 
+/* Optional split of msc_env_step: run the demand sampler of the NEXT step now (it depends only
+ * on each env's own RNG stream, not on actions), e.g. on a side stream while the policy forward
+ * runs. The following msc_env_step consumes these orders instead of generating them.
+ * No-op for the empirical sampler. */
+int msc_env_generate_demand(msc_env* env, msc_stream_t stream);
+
 /* Flat per-agent observation of the reference [E][W][L*(1+W)] = local_w || local_0..local_{W-1},
  * from the compact obs [E][W][L]. */
 int msc_env_obs_flat(const msc_env* env, const float* obs, float* flat, msc_stream_t stream);

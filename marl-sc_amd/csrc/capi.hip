@@ -1,0 +1,481 @@
+// capi.hip -- the extern "C" boundary of libmarlsc.so (include/marlsc.h).
+//
+// Host responsibilities only: validate the descriptor (the reference's EnvironmentConfig shape
+// rules, src/config/schema.py:664-890), precompute the read-only tables (home regions
+// multi_env.py:144, closest warehouses lost_sales_handler.py:36, exp(-lambda) with the host libm
+// exactly as numpy's random_poisson does, transposed outbound costs), derive per-env root seeds
+// (SeedManager.derive_env_seed, seed_manager.py:165-186), own the HBM arenas and launch the
+// kernels of env_kernels.hip / gae.hip on the caller's stream.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/marlsc.h"
+#include "env.hpp"
+#include "rng.hpp"
+
+using namespace msc;
+
+static thread_local char g_err[512] = "";
+
+static int set_err(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+#define HIP_TRY(x)                                                                   \
+  do {                                                                               \
+    hipError_t _e = (x);                                                             \
+    if (_e != hipSuccess) return set_err(-2, "%s: %s", #x, hipGetErrorString(_e));   \
+  } while (0)
+
+struct msc_env {
+  EnvConst c;
+  EnvState s;
+  int device;
+  void* tables = nullptr;   // device copy of every static table
+  void* arena = nullptr;    // persistent per-env state (checkpointed by save/load_state)
+  size_t arena_bytes = 0;
+  void* scratch = nullptr;  // per-step order buffer
+  bool demand_ready = false;  // msc_env_generate_demand ran since the last step
+};
+
+extern "C" {
+
+const char* msc_last_error(void) { return g_err; }
+int msc_abi_version(void) { return MSC_ABI_VERSION; }
+
+uint32_t msc_seedseq_u32(const uint32_t* words, int32_t n) { return ss_u32(words, n); }
+
+static int feature_dim(const msc_env_desc* d, int Lmax) {
+  const uint32_t f = d->feature_flags;
+  const int K = d->n_skus;
+  int n = 0;
+  if (f & MSC_F_INVENTORY) n += K + ((f & MSC_F_INVENTORY_AGG) ? 1 : 0);
+  if (f & MSC_F_PIPELINE) n += Lmax * K + ((f & MSC_F_PIPELINE_AGG) ? 1 : 0);
+  if (f & MSC_F_INCOMING_HOME) n += K + ((f & MSC_F_INCOMING_HOME_AGG) ? 1 : 0);
+  if (f & MSC_F_SHIPPED_HOME) n += K;
+  if (f & MSC_F_SHIPPED_AWAY) n += K + ((f & MSC_F_SHIPPED_AWAY_AGG) ? 1 : 0);
+  if (f & MSC_F_STOCKOUT) n += K;
+  if (f & MSC_F_ROLLING_MEAN) n += K + ((f & MSC_F_ROLLING_MEAN_AGG) ? 1 : 0);
+  if (f & MSC_F_FORECAST) n += K + ((f & MSC_F_FORECAST_AGG) ? 1 : 0);
+  if (f & MSC_F_DAYS_OF_SUPPLY) n += K;
+  if (f & MSC_F_NET_POSITION) n += K;
+  if (f & MSC_F_DEMAND_VARIABILITY) n += K;
+  if (f & MSC_F_DEMAND_HISTORY) n += MSC_HISTORY * K;
+  return n;
+}
+
+// Packs host vectors into one device allocation; returns device pointers by offset.
+struct TablePack {
+  std::vector<char> host;
+  size_t add(const void* p, size_t bytes) {
+    size_t off = (host.size() + 15) & ~size_t(15);
+    host.resize(off + bytes);
+    if (bytes) memcpy(host.data() + off, p, bytes);
+    return off;
+  }
+};
+
+int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t base_seed, uint32_t worker_index,
+                   int64_t env_index_offset, const uint32_t* env_seeds_host, msc_env** out) {
+  if (!d || !out) return set_err(-1, "null argument");
+  *out = nullptr;
+  if (d->abi_version != MSC_ABI_VERSION) return set_err(-1, "abi_version %d != %d", d->abi_version, MSC_ABI_VERSION);
+  const int W = d->n_warehouses, K = d->n_skus, R = d->n_regions;
+  if (W < 1 || W > MSC_MAX_W) return set_err(-1, "n_warehouses must be in [1, %d]", MSC_MAX_W);
+  if (K < 1 || K > MSC_MAX_K) return set_err(-1, "n_skus must be in [1, %d]", MSC_MAX_K);
+  if (R < 1 || R > MSC_MAX_R) return set_err(-1, "n_regions must be in [1, %d]", MSC_MAX_R);
+  if (d->episode_length < 1) return set_err(-1, "episode_length must be positive");
+  if (n_envs < 1) return set_err(-1, "n_envs must be positive");
+  if (d->max_splits < 0 || d->max_splits >= W) return set_err(-1, "max_splits must be < n_warehouses=%d", W);
+  const int WK = W * K;
+
+  // lead times -> pipeline horizon and pending ring size
+  int Lmax = 0, lact_max = 0;
+  for (int i = 0; i < WK; i++) {
+    const int elt = d->expected_lead_times[i];
+    if (elt < 1) return set_err(-1, "expected_lead_times must be positive");
+    int dev = 0;
+    if (d->lead_type == MSC_LEAD_STOCHASTIC) dev = d->max_dev_per_sku ? d->max_deviation[i % K] : d->max_deviation[0];
+    if (dev < 0) return set_err(-1, "max_deviation must be non-negative");
+    Lmax = elt > Lmax ? elt : Lmax;
+    lact_max = elt + dev > lact_max ? elt + dev : lact_max;
+  }
+  const int RING = lact_max + 1;
+  if (RING > MAX_RING) return set_err(-1, "max actual lead time %d exceeds %d", lact_max, MAX_RING - 1);
+
+  EnvConst c{};
+  c.W = W; c.K = K; c.R = R; c.T = d->episode_length; c.Lmax = Lmax; c.RING = RING;
+  c.F = feature_dim(d, Lmax);
+  c.L = c.F + (d->include_warehouse_id ? W : 0);
+  c.action_type = d->action_type; c.lead_type = d->lead_type; c.dev_per_sku = d->max_dev_per_sku;
+  c.lost_type = d->lost_type; c.scope = d->reward_scope; c.norm = d->obs_norm; c.wid = d->include_warehouse_id;
+  c.num_eval = d->num_eval_episodes; c.max_wh = d->max_splits + 1; c.demand_type = d->demand_type;
+  c.init_type = d->init_type; c.init_min = d->init_min; c.init_max = d->init_max;
+  c.hold_per_sku = d->holding_per_sku; c.pen_per_sku = d->penalty_per_sku;
+  c.flags = d->feature_flags; c.E = n_envs; c.scale = d->reward_scale; c.alpha = d->lost_alpha;
+  c.hold_scalar = d->holding_per_sku ? 0.0 : d->holding_cost[0];
+  c.pen_scalar = d->penalty_per_sku ? 0.0 : d->penalty_cost[0];
+  if (c.lost_type == MSC_LOST_COST && !(c.alpha > 0)) return set_err(-1, "cost lost-sales alpha must be > 0");
+  if (c.norm == MSC_OBS_MEANSTD && (!d->obs_mean || !d->obs_std)) return set_err(-1, "meanstd needs obs_mean/obs_std");
+  if (d->init_type == MSC_INIT_UNIFORM && (d->init_min < 0 || d->init_min > d->init_max))
+    return set_err(-1, "uniform initial inventory needs 0 <= min <= max");
+
+  // ---- static tables ---------------------------------------------------------------------
+  std::vector<double> zeros_k(K, 0.0), hold(K), pen(K), ofT((size_t)R * W), ovT((size_t)R * W);
+  for (int s = 0; s < K; s++) {
+    hold[s] = d->holding_per_sku ? d->holding_cost[s] : 0.0;
+    pen[s] = d->penalty_per_sku ? d->penalty_cost[s] : 0.0;
+  }
+  for (int w = 0; w < W; w++)
+    for (int r = 0; r < R; r++) {
+      ofT[(size_t)r * W + w] = d->outbound_fixed[(size_t)w * R + r];
+      ovT[(size_t)r * W + w] = d->outbound_variable[(size_t)w * R + r];
+    }
+  std::vector<uint32_t> home_mask(R, 0u);
+  std::vector<int32_t> closest(R, 0);
+  for (int w = 0; w < W; w++) {  // argmin over regions (first minimum), multi_env.py:144
+    int b = 0;
+    for (int r = 1; r < R; r++)
+      if (d->distances[(size_t)w * R + r] < d->distances[(size_t)w * R + b]) b = r;
+    home_mask[b] |= 1u << w;
+  }
+  for (int r = 0; r < R; r++) {  // argmin over warehouses, lost_sales_handler.py:36
+    int b = 0;
+    for (int w = 1; w < W; w++)
+      if (d->distances[(size_t)w * R + r] < d->distances[(size_t)b * R + r]) b = w;
+    closest[r] = b;
+  }
+  std::vector<double> enlam_o(R, 1.0), p_sku(R, 0.0), enlam_q((size_t)R * K, 1.0);
+  int order_cap = 1;
+  int nv = order_record_vec4(K);
+  std::vector<uint4> trec;
+  std::vector<int64_t> toff;
+  if (d->demand_type == MSC_DEMAND_POISSON) {
+    double lam_sum = 0.0;
+    for (int r = 0; r < R; r++) {
+      const double lo = d->lambda_orders[r];
+      if (!(lo >= 0.0 && lo < 10.0)) return set_err(-1, "lambda_orders[%d]=%g: only 0 <= lambda < 10 (numpy multiplication method) is supported", r, lo);
+      enlam_o[r] = exp(-lo);
+      if (lo > 0.0 && enlam_o[r] >= 1.0) return set_err(-1, "lambda_orders[%d] too small", r);
+      p_sku[r] = d->probability_skus[r];
+      lam_sum += lo;
+      for (int s = 0; s < K; s++) {
+        const double lq = d->lambda_quantity[(size_t)r * K + s];
+        if (!(lq >= 0.0 && lq < 10.0)) return set_err(-1, "lambda_quantity[%d,%d]=%g: only 0 <= lambda < 10 is supported", r, s, lq);
+        enlam_q[(size_t)r * K + s] = exp(-lq);
+      }
+    }
+    order_cap = (int)ceil(lam_sum + 12.0 * sqrt(lam_sum + 1.0) + 64.0);
+  } else if (d->demand_type == MSC_DEMAND_EMPIRICAL) {
+    const int rows = d->trace_n_rows;
+    if (rows < d->episode_length) return set_err(-1, "trace has %d timesteps < episode_length %d", rows, d->episode_length);
+    const int64_t n_ord = d->trace_offsets[rows];
+    toff.assign(d->trace_offsets, d->trace_offsets + rows + 1);
+    trec.assign((size_t)(n_ord > 0 ? n_ord : 1) * nv, make_uint4(0, 0, 0, 0));
+    for (int64_t j = 0; j < n_ord; j++) {
+      uint16_t* h = reinterpret_cast<uint16_t*>(&trec[(size_t)j * nv]);
+      const int reg = d->trace_regions[j];
+      if (reg < 0 || reg >= R) return set_err(-1, "trace region %d out of range", reg);
+      h[0] = (uint16_t)reg;
+      for (int s = 0; s < K; s++) {
+        const int q = d->trace_quantities[j * K + s];
+        if (q < 0 || q > 65535) return set_err(-1, "trace quantity %d out of range", q);
+        h[1 + s] = (uint16_t)q;
+      }
+    }
+    c.tr_rows = rows;
+  } else {
+    return set_err(-1, "unknown demand_type %d", d->demand_type);
+  }
+  c.order_cap = order_cap;
+
+  TablePack tp;
+  std::vector<int32_t> zeros_wk(WK, 0);
+  std::vector<float> zeros_f(c.F > 0 ? c.F : 1, 0.0f), ones_f(c.F > 0 ? c.F : 1, 1.0f);
+  const size_t o_act = tp.add(d->action_param, sizeof(double) * K);
+  const size_t o_init = tp.add(d->init_values ? d->init_values : zeros_wk.data(), sizeof(int32_t) * WK);
+  const size_t o_hold = tp.add(hold.data(), sizeof(double) * K);
+  const size_t o_pen = tp.add(pen.data(), sizeof(double) * K);
+  const size_t o_skw = tp.add(d->sku_weights, sizeof(double) * K);
+  const size_t o_ofT = tp.add(ofT.data(), sizeof(double) * ofT.size());
+  const size_t o_ovT = tp.add(ovT.data(), sizeof(double) * ovT.size());
+  const size_t o_inF = tp.add(d->inbound_fixed, sizeof(double) * WK);
+  const size_t o_inV = tp.add(d->inbound_variable, sizeof(double) * WK);
+  const size_t o_elo = tp.add(enlam_o.data(), sizeof(double) * R);
+  const size_t o_ps = tp.add(p_sku.data(), sizeof(double) * R);
+  const size_t o_elq = tp.add(enlam_q.data(), sizeof(double) * enlam_q.size());
+  const size_t o_elt = tp.add(d->expected_lead_times, sizeof(int32_t) * WK);
+  const size_t o_md = tp.add(d->lead_type == MSC_LEAD_STOCHASTIC ? d->max_deviation : zeros_wk.data(),
+                             sizeof(int32_t) * (d->lead_type == MSC_LEAD_STOCHASTIC && d->max_dev_per_sku ? K : 1));
+  const size_t o_hm = tp.add(home_mask.data(), sizeof(uint32_t) * R);
+  const size_t o_cl = tp.add(closest.data(), sizeof(int32_t) * R);
+  const size_t o_mean = tp.add(c.norm == MSC_OBS_MEANSTD ? d->obs_mean : zeros_f.data(), sizeof(float) * zeros_f.size());
+  const size_t o_std = tp.add(c.norm == MSC_OBS_MEANSTD ? d->obs_std : ones_f.data(), sizeof(float) * ones_f.size());
+  size_t o_toff = 0, o_trec = 0;
+  if (d->demand_type == MSC_DEMAND_EMPIRICAL) {
+    o_toff = tp.add(toff.data(), sizeof(int64_t) * toff.size());
+    o_trec = tp.add(trec.data(), sizeof(uint4) * trec.size());
+  }
+
+  HIP_TRY(hipSetDevice(device));
+  msc_env* env = new msc_env();
+  env->device = device;
+  auto fail = [&](int rc) {
+    if (env->tables) (void)hipFree(env->tables);
+    if (env->arena) (void)hipFree(env->arena);
+    if (env->scratch) (void)hipFree(env->scratch);
+    delete env;
+    return rc;
+  };
+  if (hipMalloc(&env->tables, tp.host.size()) != hipSuccess) return fail(set_err(-2, "hipMalloc(tables) failed"));
+  if (hipMemcpy(env->tables, tp.host.data(), tp.host.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_err(-2, "copy tables failed"));
+  char* tb = static_cast<char*>(env->tables);
+  c.act_param = (const double*)(tb + o_act);
+  c.init_vals = (const int32_t*)(tb + o_init);
+  c.hold = (const double*)(tb + o_hold);
+  c.pen = (const double*)(tb + o_pen);
+  c.skw = (const double*)(tb + o_skw);
+  c.ofT = (const double*)(tb + o_ofT);
+  c.ovT = (const double*)(tb + o_ovT);
+  c.inF = (const double*)(tb + o_inF);
+  c.inV = (const double*)(tb + o_inV);
+  c.enlam_o = (const double*)(tb + o_elo);
+  c.p_sku = (const double*)(tb + o_ps);
+  c.enlam_q = (const double*)(tb + o_elq);
+  c.elt = (const int32_t*)(tb + o_elt);
+  c.maxdev = (const int32_t*)(tb + o_md);
+  c.home_mask = (const uint32_t*)(tb + o_hm);
+  c.closest = (const int32_t*)(tb + o_cl);
+  c.obs_mean = (const float*)(tb + o_mean);
+  c.obs_std = (const float*)(tb + o_std);
+  if (d->demand_type == MSC_DEMAND_EMPIRICAL) {
+    c.tr_off = (const int64_t*)(tb + o_toff);
+    c.tr_rec = (const uint4*)(tb + o_trec);
+  }
+
+  // ---- persistent state arena (SoA, env fastest) -----------------------------------------
+  const int64_t E = n_envs;
+  const bool stoch = d->lead_type == MSC_LEAD_STOCHASTIC;
+  size_t off = 0;
+  auto slot = [&](size_t bytes) {
+    size_t o = off;
+    off = (off + bytes + 255) & ~size_t(255);
+    return o;
+  };
+  const size_t a_inv = slot(sizeof(int32_t) * WK * E);
+  const size_t a_rq = slot(sizeof(int32_t) * (size_t)WK * RING * E);
+  const size_t a_rl = slot(stoch ? (size_t)WK * RING * E : 1);
+  const size_t a_hist = slot(sizeof(int32_t) * (size_t)MSC_HISTORY * WK * E);
+  const size_t a_inc = slot(sizeof(int32_t) * WK * E);
+  const size_t a_fc = slot(sizeof(float) * WK * E);
+  const size_t a_rng = slot(sizeof(uint64_t) * 8 * E);
+  const size_t a_rbuf = slot(sizeof(uint32_t) * 4 * E);
+  const size_t a_t = slot(sizeof(int32_t) * E);
+  const size_t a_cnt = slot(sizeof(int32_t) * E);
+  const size_t a_orig = slot(sizeof(uint32_t) * E);
+  const size_t a_root = slot(sizeof(uint32_t) * E);
+  const size_t a_emp = slot(sizeof(int32_t) * E);
+  const size_t a_err = slot(sizeof(uint32_t) * 4);
+  env->arena_bytes = off;
+  if (hipMalloc(&env->arena, off) != hipSuccess) return fail(set_err(-2, "hipMalloc(state arena, %zu B) failed", off));
+  if (hipMemset(env->arena, 0, off) != hipSuccess) return fail(set_err(-2, "memset arena failed"));
+  char* ab = static_cast<char*>(env->arena);
+  EnvState s{};
+  s.inv = (int32_t*)(ab + a_inv);
+  s.ring_q = (int32_t*)(ab + a_rq);
+  s.ring_l = (uint8_t*)(ab + a_rl);
+  s.hist = (int32_t*)(ab + a_hist);
+  s.inc = (int32_t*)(ab + a_inc);
+  s.fc = (float*)(ab + a_fc);
+  s.rng = (uint64_t*)(ab + a_rng);
+  s.rbuf = (uint32_t*)(ab + a_rbuf);
+  s.t = (int32_t*)(ab + a_t);
+  s.counter = (int32_t*)(ab + a_cnt);
+  s.orig_root = (uint32_t*)(ab + a_orig);
+  s.root = (uint32_t*)(ab + a_root);
+  s.emp_start = (int32_t*)(ab + a_emp);
+  s.err = (uint32_t*)(ab + a_err);
+  if (d->demand_type == MSC_DEMAND_POISSON) {
+    const size_t sb = sizeof(uint4) * (size_t)nv * order_cap * E + sizeof(int32_t) * E + 256;
+    if (hipMalloc(&env->scratch, sb) != hipSuccess) return fail(set_err(-2, "hipMalloc(order buffer, %zu B) failed", sb));
+    s.orders = (uint4*)env->scratch;
+    s.n_orders = (int32_t*)((char*)env->scratch + sizeof(uint4) * (size_t)nv * order_cap * E);
+  }
+  // root seeds: explicit, or SeedSequence([base_seed, worker_index, env_index])
+  std::vector<uint32_t> roots(E);
+  std::vector<int32_t> minus1(E, -1);
+  for (int64_t i = 0; i < E; i++) {
+    if (env_seeds_host) roots[i] = env_seeds_host[i];
+    else {
+      const uint64_t idx = (uint64_t)(env_index_offset + i);
+      uint32_t words[4] = {base_seed, worker_index, (uint32_t)idx, (uint32_t)(idx >> 32)};
+      roots[i] = ss_u32(words, (idx >> 32) ? 4 : 3);
+    }
+  }
+  if (hipMemcpy(s.orig_root, roots.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(s.root, roots.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(s.emp_start, minus1.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_err(-2, "seed upload failed"));
+  if (step_lds_bytes(c) > 160 * 1024) return fail(set_err(-1, "W*K too large for the LDS budget"));
+  env->c = c;
+  env->s = s;
+  *out = env;
+  return 0;
+}
+
+void msc_env_destroy(msc_env* env) {
+  if (!env) return;
+  (void)hipSetDevice(env->device);
+  (void)hipDeviceSynchronize();
+  if (env->tables) (void)hipFree(env->tables);
+  if (env->arena) (void)hipFree(env->arena);
+  if (env->scratch) (void)hipFree(env->scratch);
+  delete env;
+}
+
+int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t* n_skus, int32_t* n_regions,
+                 int32_t* local_obs_dim, int32_t* n_features, int32_t* max_lead) {
+  if (!env) return set_err(-1, "null env");
+  if (n_envs) *n_envs = env->c.E;
+  if (n_agents) *n_agents = env->c.W;
+  if (n_skus) *n_skus = env->c.K;
+  if (n_regions) *n_regions = env->c.R;
+  if (local_obs_dim) *local_obs_dim = env->c.L;
+  if (n_features) *n_features = env->c.F;
+  if (max_lead) *max_lead = env->c.Lmax;
+  return 0;
+}
+
+int msc_env_reset(msc_env* env, const uint8_t* mask, const uint32_t* new_root_seeds, int32_t flags, float* obs,
+                  msc_stream_t stream) {
+  if (!env) return set_err(-1, "null env");
+  env->demand_ready = false;  // a reset re-seeds the demand streams
+  HIP_TRY(launch_reset(env->c, env->s, mask, new_root_seeds, flags, obs, (hipStream_t)stream));
+  return 0;
+}
+
+int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards, double* rewards_f64,
+                 uint8_t* truncated, float* final_obs, const msc_step_info* info, msc_stream_t stream) {
+  if (!env || !actions || !obs || !rewards || !truncated) return set_err(-1, "null argument");
+  const EnvConst& c = env->c;
+  hipStream_t st = (hipStream_t)stream;
+  StepIO io{};
+  io.actions = actions;
+  io.obs = obs;
+  io.rew = rewards;
+  io.rew64 = rewards_f64;
+  io.trunc = truncated;
+  io.final_obs = final_obs;
+  if (info) {
+    io.info = *info;
+    io.has_info = 1;
+    const int64_t E = c.E, W = c.W, K = c.K, R = c.R;
+    struct { void* p; size_t n; } z[] = {
+        {info->fulfilled_per_warehouse, sizeof(int32_t) * E * W * K},
+        {info->demand_per_region, sizeof(int32_t) * E * R * K},
+        {info->unfulfilled_demands, sizeof(int32_t) * E * R * K},
+        {info->shipment_counts, sizeof(int32_t) * E * W * R},
+        {info->shipment_quantities, sizeof(int32_t) * E * W * R},
+        {info->shipment_quantities_by_sku, sizeof(int32_t) * E * W * R * K},
+        {info->lost_order_counts, sizeof(int32_t) * E * R},
+        {info->lost_sales, sizeof(double) * E * W * K},
+    };
+    for (auto& q : z)
+      if (q.p) HIP_TRY(hipMemsetAsync(q.p, 0, q.n, st));
+  }
+  HIP_TRY(launch_step(c, env->s, io, !env->demand_ready, st));
+  env->demand_ready = false;
+  return 0;
+}
+
+int msc_env_generate_demand(msc_env* env, msc_stream_t stream) {
+  if (!env) return set_err(-1, "null env");
+  if (env->c.demand_type != MSC_DEMAND_POISSON) return 0;
+  HIP_TRY(launch_demand(env->c, env->s, (hipStream_t)stream));
+  env->demand_ready = true;
+  return 0;
+}
+
+int msc_env_obs_flat(const msc_env* env, const float* obs, float* flat, msc_stream_t stream) {
+  if (!env || !obs || !flat) return set_err(-1, "null argument");
+  HIP_TRY(launch_obs_flat(env->c, obs, flat, (hipStream_t)stream));
+  return 0;
+}
+
+int msc_env_read_state(const msc_env* env, int32_t* inv, int32_t* ts, int32_t* ep, uint64_t* rng) {
+  if (!env) return set_err(-1, "null env");
+  const int64_t E = env->c.E, WK = (int64_t)env->c.W * env->c.K;
+  HIP_TRY(hipDeviceSynchronize());
+  if (inv) {
+    std::vector<int32_t> soa(WK * E);
+    HIP_TRY(hipMemcpy(soa.data(), env->s.inv, sizeof(int32_t) * WK * E, hipMemcpyDeviceToHost));
+    for (int64_t e = 0; e < E; e++)
+      for (int64_t i = 0; i < WK; i++) inv[e * WK + i] = soa[i * E + e];
+  }
+  if (ts) HIP_TRY(hipMemcpy(ts, env->s.t, sizeof(int32_t) * E, hipMemcpyDeviceToHost));
+  if (ep) HIP_TRY(hipMemcpy(ep, env->s.counter, sizeof(int32_t) * E, hipMemcpyDeviceToHost));
+  if (rng) {
+    std::vector<uint64_t> r(8 * E);
+    std::vector<uint32_t> b(4 * E);
+    HIP_TRY(hipMemcpy(r.data(), env->s.rng, sizeof(uint64_t) * 8 * E, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(b.data(), env->s.rbuf, sizeof(uint32_t) * 4 * E, hipMemcpyDeviceToHost));
+    for (int64_t e = 0; e < E; e++)
+      for (int k = 0; k < 2; k++) {
+        for (int j = 0; j < 4; j++) rng[(e * 2 + k) * 6 + j] = r[(k * 4 + j) * E + e];
+        rng[(e * 2 + k) * 6 + 4] = b[(k * 2 + 0) * E + e];
+        rng[(e * 2 + k) * 6 + 5] = b[(k * 2 + 1) * E + e];
+      }
+  }
+  return 0;
+}
+
+int64_t msc_env_state_bytes(const msc_env* env) { return env ? (int64_t)env->arena_bytes : -1; }
+
+int msc_env_save_state(const msc_env* env, void* buf) {
+  if (!env || !buf) return set_err(-1, "null argument");
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(buf, env->arena, env->arena_bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int msc_env_load_state(msc_env* env, const void* buf) {
+  if (!env || !buf) return set_err(-1, "null argument");
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(env->arena, buf, env->arena_bytes, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int msc_env_check(msc_env* env) {
+  if (!env) return set_err(-1, "null env");
+  HIP_TRY(hipDeviceSynchronize());
+  uint32_t err = 0;
+  HIP_TRY(hipMemcpy(&err, env->s.err, sizeof err, hipMemcpyDeviceToHost));
+  if (err & ERR_ORDER_OVERFLOW) return set_err(-3, "per-step order buffer overflow (capacity %d)", env->c.order_cap);
+  return 0;
+}
+
+int msc_gae(const float* rewards, const float* values, const float* next_values, const uint8_t* terminated,
+            const uint8_t* truncated, int64_t n_seq, int32_t T, float gamma, float lam, float* advantages,
+            float* targets, double* stats_out, msc_stream_t stream) {
+  if (!rewards || !values || !advantages || n_seq < 0 || T < 0) return set_err(-1, "bad argument");
+  HIP_TRY(launch_gae(rewards, values, next_values, terminated, truncated, n_seq, T, gamma, lam, advantages, targets,
+                     stats_out, (hipStream_t)stream));
+  return 0;
+}
+
+int msc_adv_normalize(float* adv, int64_t n, const double* stats, msc_stream_t stream) {
+  if (!adv || !stats) return set_err(-1, "bad argument");
+  HIP_TRY(launch_adv_normalize(adv, n, stats, (hipStream_t)stream));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+// gae.hip -- advantage estimation for the rollout (RLlib 2.52.1's GAE connector, which the
+// reference enables at src/algorithms/mappo.py:154-156 / ippo.py:157-159 and post-processes with
+// src/algorithms/learners/hysteretic_learner.py:35-42).
+//
+// HBM-bound reverse scan over time: layout [T][N] (time-major) so each time row is read by
+// consecutive lanes (coalesced 16-B-per-lane when vectorised by 4 sequences per lane).
+// Per element: reward f32 + value f32 + done u8 (+ next_value on truncation rows) read,
+// advantage f32 + target f32 written = 17 B. Statistics {sum A, sum A^2, n} are reduced per
+// block in f64 and added with one f64 atomic per block for the cross-rank standardisation.
+#include <hip/hip_runtime.h>
+
+#include "env.hpp"
+
+namespace msc {
+
+constexpr int GAE_BS = 256;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(GAE_BS) void gae_kernel(const float* __restrict__ r, const float* __restrict__ v,
+                                                     const float* __restrict__ nv, const uint8_t* __restrict__ term,
+                                                     const uint8_t* __restrict__ trunc, int64_t N, int32_t T,
+                                                     float gamma, float lam, float* __restrict__ adv,
+                                                     float* __restrict__ tgt, double* __restrict__ stats) {
+  __shared__ double red[2][GAE_BS / 64];
+  const int64_t n = (int64_t)blockIdx.x * GAE_BS + threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  if (n < N) {
+    float a = 0.0f;
+    float v_next = v[(int64_t)T * N + n];
+    const float gl = gamma * lam;
+    for (int t = T - 1; t >= 0; --t) {
+      const int64_t i = (int64_t)t * N + n;
+      const float vt = v[i];
+      const bool te = term && term[i];
+      const bool tr = trunc && trunc[i];
+      float boot = tr ? (nv ? nv[i] : 0.0f) : v_next;
+      if (te) boot = 0.0f;
+      const float delta = r[i] + gamma * boot - vt;
+      a = delta + ((te || tr) ? 0.0f : gl * a);
+      adv[i] = a;
+      if (tgt) tgt[i] = a + vt;
+      s1 += (double)a;
+      s2 += (double)a * (double)a;
+      v_next = vt;
+    }
+  }
+  if (stats) {
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    const int wid = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    if (ln == 0) {
+      red[0][wid] = s1;
+      red[1][wid] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double a1 = 0.0, a2 = 0.0;
+      for (int k = 0; k < GAE_BS / 64; k++) {
+        a1 += red[0][k];
+        a2 += red[1][k];
+      }
+      const int64_t cnt = (N - (int64_t)blockIdx.x * GAE_BS) < GAE_BS ? (N - (int64_t)blockIdx.x * GAE_BS) : GAE_BS;
+      atomicAdd(&stats[0], a1);
+      atomicAdd(&stats[1], a2);
+      atomicAdd(&stats[2], (double)cnt * (double)T);
+    }
+  }
+}
+
+__global__ void adv_norm_kernel(float* __restrict__ adv, int64_t n, const double* __restrict__ st) {
+  const double cnt = st[2] > 0 ? st[2] : 1.0;
+  const double mean = st[0] / cnt;
+  double var = st[1] / cnt - mean * mean;
+  var = var > 0 ? var : 0.0;
+  double sd = sqrt(var);
+  sd = sd > 1e-4 ? sd : 1e-4;
+  const float m = (float)mean, inv = (float)(1.0 / sd);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    adv[i] = (adv[i] - m) * inv;
+}
+
+hipError_t launch_gae(const float* r, const float* v, const float* nv, const uint8_t* term, const uint8_t* trunc,
+                      int64_t N, int32_t T, float gamma, float lam, float* adv, float* tgt, double* stats,
+                      hipStream_t st) {
+  if (N == 0) return hipSuccess;
+  const int64_t blocks = (N + GAE_BS - 1) / GAE_BS;
+  hipLaunchKernelGGL(gae_kernel, dim3((unsigned)blocks), dim3(GAE_BS), 0, st, r, v, nv, term, trunc, N, T, gamma,
+                     lam, adv, tgt, stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_adv_normalize(float* adv, int64_t n, const double* stats, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(adv_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, st, adv, n, stats);
+  return hipGetLastError();
+}
+
+}  // namespace msc

@@ -1,0 +1,172 @@
+// rng.hpp -- numpy-2.x-compatible random streams for the device (and host) side of libmarlsc.
+//
+// The reference draws all env randomness from numpy Generators created by its SeedManager
+// (src/utils/seed_manager.py:63-78, 100-120, 207-224): SeedSequence pools -> PCG64 -> random(),
+// poisson() (multiplication method below lam = 10), integers() (32-bit buffered Lemire).
+// Restated here on 64-bit limbs so a gfx950 lane advances a 128-bit LCG with 13 integer
+// multiplies and no 128-bit emulation library. Every function is bit-exact with numpy; the
+// parity tests compare the resulting PCG64 states after every step.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define MSC_HD __host__ __device__ __forceinline__
+#else
+#define MSC_HD inline
+#endif
+
+namespace msc {
+
+// ---- SeedSequence (numpy/random/bit_generator.pyx) ------------------------------------------
+constexpr uint32_t SS_INIT_A = 0x43b0d7e5u, SS_MULT_A = 0x931e8875u;
+constexpr uint32_t SS_INIT_B = 0x8b51f9ddu, SS_MULT_B = 0x58f38dedu;
+constexpr uint32_t SS_MIX_L = 0xca01f9ddu, SS_MIX_R = 0x4973f715u;
+
+MSC_HD uint32_t ss_hashmix(uint32_t v, uint32_t& hc) {
+  v ^= hc;
+  hc *= SS_MULT_A;
+  v *= hc;
+  return v ^ (v >> 16);
+}
+MSC_HD uint32_t ss_mix(uint32_t x, uint32_t y) {
+  uint32_t r = SS_MIX_L * x - SS_MIX_R * y;
+  return r ^ (r >> 16);
+}
+// Pool of SeedSequence(entropy[0..n)) or, with spawn key k >= 0,
+// SeedSequence(entropy, spawn_key=(k,)) (entropy zero-padded to 4 words first).
+MSC_HD void ss_pool(const uint32_t* ent, int n_ent, int spawn_key, uint32_t pool[4]) {
+  uint32_t buf[6];
+  int n = 0;
+  for (int i = 0; i < n_ent && i < 5; i++) buf[n++] = ent[i];
+  if (spawn_key >= 0) {
+    while (n < 4) buf[n++] = 0u;
+    buf[n++] = (uint32_t)spawn_key;
+  }
+  uint32_t hc = SS_INIT_A;
+#pragma unroll
+  for (int i = 0; i < 4; i++) pool[i] = ss_hashmix(i < n ? buf[i] : 0u, hc);
+#pragma unroll
+  for (int s = 0; s < 4; s++)
+#pragma unroll
+    for (int d = 0; d < 4; d++)
+      if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], hc));
+  for (int s = 4; s < n; s++)
+#pragma unroll
+    for (int d = 0; d < 4; d++) pool[d] = ss_mix(pool[d], ss_hashmix(buf[s], hc));
+}
+MSC_HD void ss_generate(const uint32_t pool[4], uint32_t* out, int n_words) {
+  uint32_t hc = SS_INIT_B;
+  for (int i = 0; i < n_words; i++) {
+    uint32_t v = pool[i & 3] ^ hc;
+    hc *= SS_MULT_B;
+    v *= hc;
+    out[i] = v ^ (v >> 16);
+  }
+}
+MSC_HD uint32_t ss_u32(const uint32_t* words, int n) {
+  uint32_t pool[4], o;
+  ss_pool(words, n, -1, pool);
+  ss_generate(pool, &o, 1);
+  return o;
+}
+
+// ---- PCG64 (XSL-RR 128/64) ------------------------------------------------------------------
+constexpr uint64_t PCG_MUL_HI = 2549297995355413924ULL;
+constexpr uint64_t PCG_MUL_LO = 4865540595714422341ULL;
+
+struct Pcg64 {
+  uint64_t s_hi, s_lo, i_hi, i_lo;  // state, increment
+  uint32_t has32, u32;               // numpy's buffered upper half for next_uint32
+};
+
+MSC_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+MSC_HD void pcg_step(Pcg64& r) {
+  uint64_t lo = r.s_lo * PCG_MUL_LO;
+  uint64_t hi = r.s_hi * PCG_MUL_LO + r.s_lo * PCG_MUL_HI + mulhi64(r.s_lo, PCG_MUL_LO);
+  uint64_t nlo = lo + r.i_lo;
+  hi += r.i_hi + (nlo < lo ? 1u : 0u);
+  r.s_lo = nlo;
+  r.s_hi = hi;
+}
+MSC_HD uint64_t pcg_next64(Pcg64& r) {
+  pcg_step(r);
+  uint64_t x = r.s_hi ^ r.s_lo;
+  unsigned rot = (unsigned)(r.s_hi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+MSC_HD uint32_t pcg_next32(Pcg64& r) {
+  if (r.has32) {
+    r.has32 = 0;
+    return r.u32;
+  }
+  uint64_t v = pcg_next64(r);
+  r.has32 = 1;
+  r.u32 = (uint32_t)(v >> 32);
+  return (uint32_t)v;
+}
+MSC_HD double pcg_double(Pcg64& r) { return (double)(pcg_next64(r) >> 11) * (1.0 / 9007199254740992.0); }
+
+// PCG64(SeedSequence pool): generate_state(4, uint64) = {seed_hi, seed_lo, inc_hi, inc_lo}
+MSC_HD void pcg_seed_pool(Pcg64& r, const uint32_t pool[4]) {
+  uint32_t w[8];
+  ss_generate(pool, w, 8);
+  uint64_t s0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), s1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  uint64_t q0 = (uint64_t)w[4] | ((uint64_t)w[5] << 32), q1 = (uint64_t)w[6] | ((uint64_t)w[7] << 32);
+  // inc = (initseq << 1) | 1 over 128 bits
+  r.i_hi = (q0 << 1) | (q1 >> 63);
+  r.i_lo = (q1 << 1) | 1u;
+  r.s_hi = 0;
+  r.s_lo = 0;
+  pcg_step(r);
+  uint64_t lo = r.s_lo + s1;
+  r.s_hi += s0 + (lo < s1 ? 1u : 0u);
+  r.s_lo = lo;
+  pcg_step(r);
+  r.has32 = 0;
+  r.u32 = 0;
+}
+// Generator of SeedManager child `key` of root seed `root` (spawn_key=(key,))
+MSC_HD void pcg_seed_child(Pcg64& r, uint32_t root, int key) {
+  uint32_t pool[4];
+  ss_pool(&root, 1, key, pool);
+  pcg_seed_pool(r, pool);
+}
+
+// random_poisson for 0 <= lam < 10: multiplication method; enlam = exp(-lam) from the host libm.
+MSC_HD int poisson_mult(Pcg64& r, double enlam) {
+  int x = 0;
+  double prod = 1.0;
+  for (;;) {
+    prod *= pcg_double(r);
+    if (prod > enlam) x += 1;
+    else return x;
+  }
+}
+
+// Generator.integers(low, high_exclusive) for ranges < 2^32 (buffered 32-bit Lemire).
+MSC_HD int64_t bounded_int(Pcg64& r, int64_t low, int64_t high_excl) {
+  uint32_t rng = (uint32_t)(high_excl - 1 - low);
+  if (rng == 0) return low;
+  if (rng == 0xFFFFFFFFu) return low + (int64_t)pcg_next32(r);
+  uint32_t rng_excl = rng + 1u;
+  uint64_t m = (uint64_t)pcg_next32(r) * rng_excl;
+  uint32_t left = (uint32_t)m;
+  if (left < rng_excl) {
+    uint32_t thr = (0xFFFFFFFFu - rng) % rng_excl;
+    while (left < thr) {
+      m = (uint64_t)pcg_next32(r) * rng_excl;
+      left = (uint32_t)m;
+    }
+  }
+  return low + (int64_t)(m >> 32);
+}
+
+}  // namespace msc

@@ -1,0 +1,175 @@
+"""VecInventoryEnv: E copies of the reference's InventoryEnvironment resident on one MI355X.
+
+Thin host wrapper over the C ABI of libmarlsc.so (include/marlsc.h). torch provides device
+memory and the current HIP stream; all environment arithmetic runs in the HIP kernels
+(csrc/env_kernels.hip). There is no CPU fallback: without the built library this raises.
+
+Semantics per env follow `InventoryEnvironment` (src/environment/envs/multi_env.py:192-366)
+with RLlib's EnvRunner loop folded in: an env whose episode truncates is reset inside the same
+`step()` (its terminal observation is returned in `final_obs`), exactly as the runner calls
+`reset()` after a truncation. Per-env root seeds are `SeedManager.derive_env_seed(base_seed,
+worker_index, env_index)` (seed_manager.py:165-186, used by the env factory at
+src/algorithms/base.py:413-419), so env `g` has the same trajectory however envs are sharded.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+
+from . import abi
+from .seeding import default_train_seed
+from .spec import EnvSpec
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class VecInventoryEnv:
+    def __init__(self, env_config: Any, n_envs: int, *, env_meta: Optional[Dict[str, Any]] = None,
+                 device: int = 0, base_seed: Optional[int] = None, worker_index: int = 0,
+                 env_index_offset: int = 0, env_seeds=None, allow_nr_ne_nw: bool = True,
+                 demand_trace: Any = None, spec: Optional[EnvSpec] = None):
+        self.spec = spec if spec is not None else EnvSpec.from_config(
+            env_config, env_meta, allow_nr_ne_nw=allow_nr_ne_nw, demand_trace=demand_trace)
+        self.n_envs = int(n_envs)
+        self.device = torch.device("cuda", device)
+        self.base_seed = default_train_seed() if base_seed is None else int(base_seed)
+        L = abi.lib()
+        desc = self.spec.to_desc()
+        seeds = None
+        if env_seeds is not None:
+            arr = np.ascontiguousarray(env_seeds, dtype=np.uint32)
+            assert arr.shape == (self.n_envs,)
+            seeds = arr.ctypes.data_as(C.POINTER(C.c_uint32))
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            abi.check(L.msc_env_create(C.byref(desc), device, self.n_envs, self.base_seed & 0xFFFFFFFF,
+                                       worker_index, env_index_offset, seeds, C.byref(h)))
+        self._h = h
+        n = C.c_int64()
+        W, K, R, Lo, F, lm = (C.c_int32() for _ in range(6))
+        abi.check(L.msc_env_dims(h, C.byref(n), C.byref(W), C.byref(K), C.byref(R), C.byref(Lo), C.byref(F), C.byref(lm)))
+        self.W, self.K, self.R, self.L, self.F = W.value, K.value, R.value, Lo.value, F.value
+        assert self.L == self.spec.local_obs_dim
+        E, dev = self.n_envs, self.device
+        self.obs = torch.zeros((E, self.W, self.L), dtype=torch.float32, device=dev)
+        self.final_obs = torch.zeros_like(self.obs)
+        self.rewards = torch.zeros((E, self.W), dtype=torch.float32, device=dev)
+        self.rewards_f64 = torch.zeros((E, self.W), dtype=torch.float64, device=dev)
+        self.truncated = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self._info = None
+
+    # ---- properties mirroring the reference object ------------------------------------------
+    @property
+    def n_agents(self) -> int:
+        return self.W
+
+    @property
+    def local_obs_dim(self) -> int:
+        return self.L
+
+    @property
+    def global_obs_dim(self) -> int:
+        return self.L * self.W
+
+    @property
+    def agents(self):
+        return [f"warehouse_{i}" for i in range(self.W)]
+
+    # ---- API ---------------------------------------------------------------------------------
+    def reset(self, mask: Optional[torch.Tensor] = None, root_seeds: Optional[torch.Tensor] = None,
+              eval_restart: bool = False) -> torch.Tensor:
+        """Reset envs (mask: [E] u8/bool on device, None = all). root_seeds ([E] int on device)
+        follows reset(seed=...) of an env built without a seed (update_root_seed)."""
+        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        s = None if root_seeds is None else root_seeds.to(device=self.device, dtype=torch.int64).to(torch.int32).contiguous()
+        flags = abi.RESET_EVAL_RESTART if eval_restart else 0
+        abi.check(abi.lib().msc_env_reset(self._h, _p(m), _p(s), flags, _p(self.obs), _stream()))
+        return self.obs
+
+    def step(self, actions: torch.Tensor, *, want_final_obs: bool = True, want_f64: bool = False,
+             info: Optional[Dict[str, torch.Tensor]] = None):
+        """actions [E, W, K] float32 on the device. Returns (obs [E,W,L], rewards [E,W],
+        truncated [E] bool-as-u8, final_obs [E,W,L] or None). Returned tensors are internal
+        buffers, overwritten by the next call."""
+        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if actions.shape != (self.n_envs, self.W, self.K):
+            raise ValueError(f"actions must have shape {(self.n_envs, self.W, self.K)}, got {tuple(actions.shape)}")
+        si = None
+        if info is not None:
+            s = abi.MscStepInfo()
+            for k, v in info.items():
+                setattr(s, k, C.cast(C.c_void_p(v.data_ptr()), C.POINTER(C.c_double if v.dtype == torch.float64 else C.c_int32)))
+            si = C.byref(s)
+        abi.check(abi.lib().msc_env_step(
+            self._h, _p(actions), _p(self.obs), _p(self.rewards), _p(self.rewards_f64) if want_f64 else None,
+            _p(self.truncated), _p(self.final_obs) if want_final_obs else None, si, _stream()))
+        return self.obs, self.rewards, self.truncated, (self.final_obs if want_final_obs else None)
+
+    def generate_demand(self) -> None:
+        """Draw the next step's demand now (see msc_env_generate_demand); overlappable."""
+        abi.check(abi.lib().msc_env_generate_demand(self._h, _stream()))
+
+    def alloc_info(self) -> Dict[str, torch.Tensor]:
+        """Device buffers for msc_step_info (the reference's collect_step_info dict)."""
+        E, W, K, R = self.n_envs, self.W, self.K, self.R
+        shapes = {"inventory_before": (W, K), "pending_total": (W, K), "order_quantities": (W, K),
+                  "demand_per_region": (R, K), "fulfilled_per_warehouse": (W, K), "unfulfilled_demands": (R, K),
+                  "shipment_counts": (W, R), "shipment_quantities": (W, R), "shipment_quantities_by_sku": (W, R, K),
+                  "lost_order_counts": (R,), "n_orders": (), "lost_sales": (W, K), "costs": (4, W)}
+        return {k: torch.zeros((E,) + sh, dtype=torch.float64 if k in ("lost_sales", "costs") else torch.int32,
+                               device=self.device) for k, sh in shapes.items()}
+
+    def obs_flat(self, obs: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Reference layout [E, W, L*(1+W)] = local_w || concat_j local_j (multi_env.py:566-573)."""
+        obs = self.obs if obs is None else obs
+        if out is None:
+            out = torch.empty((self.n_envs, self.W, self.L * (1 + self.W)), dtype=torch.float32, device=self.device)
+        abi.check(abi.lib().msc_env_obs_flat(self._h, _p(obs), _p(out), _stream()))
+        return out
+
+    def read_state(self) -> Dict[str, np.ndarray]:
+        E = self.n_envs
+        inv = np.zeros((E, self.W, self.K), np.int32)
+        ts = np.zeros(E, np.int32)
+        ep = np.zeros(E, np.int32)
+        rng = np.zeros((E, 2, 6), np.uint64)
+        abi.check(abi.lib().msc_env_read_state(self._h, inv.ctypes.data_as(C.c_void_p), ts.ctypes.data_as(C.c_void_p),
+                                               ep.ctypes.data_as(C.c_void_p), rng.ctypes.data_as(C.c_void_p)))
+        return {"inventory": inv, "timestep": ts, "episode_counter": ep, "rng": rng}
+
+    def save_state(self) -> bytes:
+        n = abi.lib().msc_env_state_bytes(self._h)
+        buf = (C.c_char * n)()
+        abi.check(abi.lib().msc_env_save_state(self._h, buf))
+        return bytes(buf)
+
+    def load_state(self, blob: bytes) -> None:
+        n = abi.lib().msc_env_state_bytes(self._h)
+        if len(blob) != n:
+            raise ValueError(f"state blob has {len(blob)} bytes, expected {n}")
+        buf = (C.c_char * n).from_buffer_copy(blob)
+        abi.check(abi.lib().msc_env_load_state(self._h, buf))
+
+    def check(self) -> None:
+        abi.check(abi.lib().msc_env_check(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            abi.lib().msc_env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

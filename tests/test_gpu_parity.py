@@ -1,0 +1,239 @@
+"""GPU parity: the HIP path (libmarlsc via VecInventoryEnv) against the reference's golden vectors
+and against the C oracle on larger seeded batches. Bar: bit-exact integer state, observations and
+PCG64 states; rewards within 1e-6 absolute (north star: 1e-5)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle as orc  # noqa: E402
+from golden_util import COST_KEYS, ENV_FIXTURES, INFO_MAP, load, spec_of  # noqa: E402
+from marlsc import make_synthetic_env_config  # noqa: E402
+from marlsc.spec import EnvSpec  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+REW_ATOL = 1e-6
+
+
+def _vec(spec, E, **kw):
+    from marlsc.vec_env import VecInventoryEnv
+    return VecInventoryEnv(None, E, spec=spec, device=0, **kw)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ENV_FIXTURES)
+def test_gpu_matches_reference_golden(name):
+    d, meta = load(name)
+    spec = spec_of(d, meta)
+    E, S = meta["n_envs"], meta["n_steps"]
+    env = _vec(spec, E, env_seeds=meta["env_seeds"])
+    np.testing.assert_array_equal(_np(env.reset()), d["reset_obs"][:, 0])
+    st = env.read_state()
+    np.testing.assert_array_equal(st["inventory"], d["reset_inventory"][:, 0])
+    np.testing.assert_array_equal(st["rng"][:, 0], d["reset_rng_demand"][:, 0])
+    np.testing.assert_array_equal(st["rng"][:, 1], d["reset_rng_lead"][:, 0])
+    reset_steps = list(d["reset_step"][0])
+    for t in range(S):
+        info = env.alloc_info()
+        obs, rew, tr, fo = env.step(torch.from_numpy(d["actions"][:, t]).cuda(), want_f64=True, info=info)
+        h = {k: _np(v) for k, v in info.items()}
+        for fk, ik in INFO_MAP.items():
+            if fk == "lost_sales":
+                np.testing.assert_allclose(h[ik], d[fk][:, t], rtol=1e-9, atol=1e-9, err_msg=f"{name} t={t} {fk}")
+            else:
+                np.testing.assert_array_equal(h[ik], d[fk][:, t], err_msg=f"{name} t={t} {fk}")
+        for c, ck in enumerate(COST_KEYS):
+            np.testing.assert_allclose(h["costs"][:, c], d[ck][:, t], rtol=1e-9, atol=1e-7, err_msg=f"{name} t={t} {ck}")
+        np.testing.assert_allclose(_np(env.rewards_f64), d["rewards"][:, t], rtol=0, atol=REW_ATOL)
+        np.testing.assert_allclose(_np(rew), d["rewards"][:, t].astype(np.float32), rtol=1e-6, atol=1e-5)
+        trn = _np(tr).astype(bool)
+        assert np.array_equal(trn, d["trunc"][:, t])
+        np.testing.assert_array_equal(_np(fo) if trn.any() else _np(obs), d["obs"][:, t], err_msg=f"{name} t={t} obs")
+        if trn.any() and (t + 1) in reset_steps:
+            np.testing.assert_array_equal(_np(obs), d["reset_obs"][:, reset_steps.index(t + 1)])
+        if not trn.any():
+            st = env.read_state()
+            np.testing.assert_array_equal(st["inventory"], d["inv_after"][:, t])
+            np.testing.assert_array_equal(st["rng"][:, 0], d["rng_demand"][:, t])
+            np.testing.assert_array_equal(st["rng"][:, 1], d["rng_lead"][:, t])
+    env.check()
+
+
+def _lockstep(spec, E, steps, seed=0, base_seed=777, check_every=1):
+    env = _vec(spec, E, base_seed=base_seed)
+    ref = orc.OracleEnv(spec, E, base_seed=base_seed)
+    np.testing.assert_array_equal(_np(env.reset()), ref.reset())
+    rng = np.random.default_rng(seed)
+    for t in range(steps):
+        a = rng.uniform(-1, 1, size=(E, spec.W, spec.K)).astype(np.float32)
+        og, _, tg, fg = env.step(torch.from_numpy(a).cuda(), want_f64=True)
+        orr, rr, tr, fr = ref.step(a, final_obs=True, n_threads=8)
+        assert np.array_equal(_np(tg).astype(bool), tr)
+        np.testing.assert_allclose(_np(env.rewards_f64), rr, rtol=0, atol=REW_ATOL, err_msg=f"t={t}")
+        np.testing.assert_array_equal(_np(og), orr, err_msg=f"obs t={t}")
+        if tr.any():
+            np.testing.assert_array_equal(_np(fg)[tr], fr[tr], err_msg=f"final obs t={t}")
+        if t % check_every == 0:
+            sg, sr = env.read_state(), ref.read_state()
+            np.testing.assert_array_equal(sg["inventory"], sr["inventory"])
+            np.testing.assert_array_equal(sg["rng"], sr["rng"])
+            np.testing.assert_array_equal(sg["timestep"], sr["timestep"])
+    env.check()
+    return env, ref
+
+
+def test_bench_config_vs_oracle_across_episode_boundary():
+    # BASELINE configs 2-4 shape (8 x 64 x 5), 512 envs, 110 steps (one in-kernel auto-reset)
+    cfg = make_synthetic_env_config(8, 64, 5)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 512, 110, check_every=10)
+
+
+def test_c5_shape_vs_oracle():
+    cfg = make_synthetic_env_config(16, 256, 5, episode_length=12)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 64, 15, check_every=5)
+
+
+@pytest.mark.parametrize("name", ["c8_split", "variant_a", "variant_b", "variant_c", "repo_3wh5sku"])
+def test_variants_vs_oracle_many_envs(name):
+    d, meta = load(name)
+    _lockstep(spec_of(d, meta), 300, 70, seed=3, check_every=7)
+
+
+def test_generate_demand_split_equals_fused():
+    cfg = make_synthetic_env_config(8, 64, 5)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    a, b = _vec(spec, 256, base_seed=5), _vec(spec, 256, base_seed=5)
+    a.reset(), b.reset()
+    rng = np.random.default_rng(1)
+    side = torch.cuda.Stream()
+    for t in range(30):
+        act = torch.from_numpy(rng.uniform(-1, 1, (256, 8, 5)).astype(np.float32)).cuda()
+        oa = a.step(act)[0].clone()
+        with torch.cuda.stream(side):
+            b.generate_demand()
+        torch.cuda.current_stream().wait_stream(side)
+        ob = b.step(act)[0]
+        assert torch.equal(oa, ob)
+
+
+def test_sharding_invariance():
+    # env g has the same trajectory whether it lives in one batch or in a shard (global env ids)
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=15)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    full = _vec(spec, 128, base_seed=99)
+    lo = _vec(spec, 64, base_seed=99, env_index_offset=0)
+    hi = _vec(spec, 64, base_seed=99, env_index_offset=64)
+    full.reset(), lo.reset(), hi.reset()
+    rng = np.random.default_rng(2)
+    for _ in range(20):
+        act = torch.from_numpy(rng.uniform(-1, 1, (128, 8, 5)).astype(np.float32)).cuda()
+        of = full.step(act)[0].clone()
+        ol = lo.step(act[:64].contiguous())[0].clone()
+        oh = hi.step(act[64:].contiguous())[0].clone()
+        assert torch.equal(of, torch.cat([ol, oh]))
+
+
+def test_save_load_state_roundtrip():
+    d, meta = load("variant_b")
+    env = _vec(spec_of(d, meta), 64, base_seed=3)
+    env.reset()
+    rng = np.random.default_rng(4)
+    acts = [torch.from_numpy(rng.uniform(-1, 1, (64, env.W, env.K)).astype(np.float32)).cuda() for _ in range(12)]
+    for a in acts[:4]:
+        env.step(a)
+    blob = env.save_state()
+    first = [env.step(a)[0].clone() for a in acts[4:]]
+    env.load_state(blob)
+    second = [env.step(a)[0].clone() for a in acts[4:]]
+    for x, y in zip(first, second):
+        assert torch.equal(x, y)
+
+
+def test_masked_reset_and_root_seeds():
+    d, meta = load("c1_2x4x2")
+    spec = spec_of(d, meta)
+    env = _vec(spec, 8, base_seed=11)
+    ref = orc.OracleEnv(spec, 8, base_seed=11)
+    env.reset(), ref.reset()
+    rng = np.random.default_rng(5)
+    for _ in range(3):
+        a = rng.uniform(-1, 1, (8, spec.W, spec.K)).astype(np.float32)
+        env.step(torch.from_numpy(a).cuda())
+        ref.step(a)
+    mask = np.array([1, 0, 1, 0, 0, 0, 0, 1], np.uint8)
+    seeds = np.arange(8, dtype=np.uint32) * 1000 + 17
+    og = _np(env.reset(mask=torch.from_numpy(mask).cuda(), root_seeds=torch.from_numpy(seeds.astype(np.int64)).cuda()))
+    orr = ref.reset(mask=mask, new_root_seeds=seeds)
+    np.testing.assert_array_equal(og[mask == 1], orr[mask == 1])
+    for _ in range(5):
+        a = rng.uniform(-1, 1, (8, spec.W, spec.K)).astype(np.float32)
+        o1 = _np(env.step(torch.from_numpy(a).cuda())[0])
+        o2, _, _, _ = ref.step(a)
+        np.testing.assert_array_equal(o1, o2)
+
+
+def test_obs_flat_layout():
+    d, meta = load("c3_8x64x5")
+    spec = spec_of(d, meta)
+    env = _vec(spec, 3, env_seeds=meta["env_seeds"])
+    env.reset()
+    env.step(torch.from_numpy(d["actions"][:, 0]).cuda())
+    loc = _np(env.obs)
+    flat = _np(env.obs_flat())
+    for w in range(spec.W):
+        np.testing.assert_array_equal(flat[:, w, :spec.local_obs_dim], loc[:, w])
+        np.testing.assert_array_equal(flat[:, w, spec.local_obs_dim:], loc.reshape(3, -1))
+
+
+def test_gae_kernel_vs_numpy():
+    import ctypes as C
+    from gae_ref import gae, normalize
+    from marlsc import abi
+    rng = np.random.default_rng(0)
+    T, N = 100, 5000
+    r = rng.normal(size=(T, N)).astype(np.float32)
+    v = rng.normal(size=(T + 1, N)).astype(np.float32)
+    nv = rng.normal(size=(T, N)).astype(np.float32)
+    te = (rng.random((T, N)) < 0.01).astype(np.uint8)
+    tr = np.zeros((T, N), np.uint8)
+    tr[49] = 1
+    dev = {k: torch.from_numpy(x).cuda() for k, x in dict(r=r, v=v, nv=nv, te=te, tr=tr).items()}
+    adv = torch.empty((T, N), device="cuda")
+    tgt = torch.empty((T, N), device="cuda")
+    stats = torch.zeros(3, dtype=torch.float64, device="cuda")
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    abi.check(abi.lib().msc_gae(p(dev["r"]), p(dev["v"]), p(dev["nv"]), p(dev["te"]), p(dev["tr"]), N, T,
+                                C.c_float(0.99), C.c_float(0.95), p(adv), p(tgt), p(stats), None))
+    a_ref, t_ref = gae(r.astype(np.float64), v.astype(np.float64), nv.astype(np.float64), te, tr, 0.99, 0.95)
+    np.testing.assert_allclose(_np(adv), a_ref, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(tgt), t_ref, rtol=1e-4, atol=1e-4)
+    s = _np(stats)
+    assert s[2] == T * N
+    np.testing.assert_allclose(s[0], a_ref.sum(), rtol=1e-5)
+    abi.check(abi.lib().msc_adv_normalize(p(adv), T * N, p(stats), None))
+    np.testing.assert_allclose(_np(adv), normalize(a_ref), rtol=1e-3, atol=1e-3)
+
+
+def test_pettingzoo_adapter_matches_golden():
+    from marlsc.env import InventoryEnvironment
+    d, meta = load("repo_3wh5sku")
+    env_meta = dict(meta["env_meta"])
+    env = InventoryEnvironment(meta["config"], seed=meta["env_seeds"][0], env_meta=env_meta)
+    env.collect_step_info = True
+    obs, _ = env.reset()
+    L = env._compute_local_obs_dim()
+    np.testing.assert_array_equal(np.stack([obs[a][:L] for a in env.agents]), d["reset_obs"][0, 0])
+    for t in range(meta["n_steps"]):
+        acts = {a: d["actions"][0, t, i] for i, a in enumerate(env.agents)}
+        obs, rew, term, trunc, infos = env.step(acts)
+        np.testing.assert_array_equal(np.stack([obs[a][:L] for a in env.agents]), d["obs"][0, t])
+        np.testing.assert_allclose([rew[a] for a in env.agents], d["rewards"][0, t], atol=REW_ATOL, rtol=0)
+        np.testing.assert_array_equal(infos[env.agents[0]]["shipment_quantities_by_sku"], d["shipment_quantities_by_sku"][0, t])
+        assert obs[env.agents[0]].shape == env.observation_space(env.agents[0]).shape
+        if trunc[env.agents[0]]:
+            obs, _ = env.reset()
