@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -44,6 +45,7 @@ struct msc_env {
   size_t arena_bytes = 0;
   void* scratch = nullptr;  // per-step order buffer
   bool demand_ready = false;  // msc_env_generate_demand ran since the last step
+  DevEnv* dev = nullptr;      // device copy of {c, s}
 };
 
 extern "C" {
@@ -162,14 +164,15 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     double lam_sum = 0.0;
     for (int r = 0; r < R; r++) {
       const double lo = d->lambda_orders[r];
-      if (!(lo >= 0.0 && lo < 10.0)) return set_err(-1, "lambda_orders[%d]=%g: only 0 <= lambda < 10 (numpy multiplication method) is supported", r, lo);
+      // PositiveFloat in the reference schema (schema.py:191); >= 10 would be numpy's PTRS branch
+      if (!(lo > 0.0 && lo < 10.0)) return set_err(-1, "lambda_orders[%d]=%g: only 0 < lambda < 10 (numpy multiplication method) is supported", r, lo);
       enlam_o[r] = exp(-lo);
       if (lo > 0.0 && enlam_o[r] >= 1.0) return set_err(-1, "lambda_orders[%d] too small", r);
       p_sku[r] = d->probability_skus[r];
       lam_sum += lo;
       for (int s = 0; s < K; s++) {
         const double lq = d->lambda_quantity[(size_t)r * K + s];
-        if (!(lq >= 0.0 && lq < 10.0)) return set_err(-1, "lambda_quantity[%d,%d]=%g: only 0 <= lambda < 10 is supported", r, s, lq);
+        if (!(lq > 0.0 && lq < 10.0)) return set_err(-1, "lambda_quantity[%d,%d]=%g: only 0 < lambda < 10 is supported", r, s, lq);
         enlam_q[(size_t)r * K + s] = exp(-lq);
       }
     }
@@ -196,6 +199,12 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     return set_err(-1, "unknown demand_type %d", d->demand_type);
   }
   c.order_cap = order_cap;
+  {
+    const char* abl = getenv("MSC_ABLATE");
+    c.ablate = abl ? atoi(abl) : 0;
+    const char* impl = getenv("MSC_DEMAND_IMPL");
+    c.demand_impl = !impl ? 0 : strcmp(impl, "nested") == 0 ? 1 : strcmp(impl, "flat_branchy") == 0 ? 2 : 0;
+  }
 
   TablePack tp;
   std::vector<int32_t> zeros_wk(WK, 0);
@@ -232,6 +241,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     if (env->tables) (void)hipFree(env->tables);
     if (env->arena) (void)hipFree(env->arena);
     if (env->scratch) (void)hipFree(env->scratch);
+    if (env->dev) (void)hipFree(env->dev);
     delete env;
     return rc;
   };
@@ -325,9 +335,17 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       hipMemcpy(s.root, roots.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(s.emp_start, minus1.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice) != hipSuccess)
     return fail(set_err(-2, "seed upload failed"));
-  if (step_lds_bytes(c) > 160 * 1024) return fail(set_err(-1, "W*K too large for the LDS budget"));
+  c.cost_lds = step_lds_bytes_for(c, true) <= LDS_BUDGET ? 1 : 0;
+  c.dem_lds = (size_t)(2 + K) * R * sizeof(double) <= 64 * 1024 ? 1 : 0;
+  if (step_lds_bytes(c) > LDS_BUDGET) return fail(set_err(-1, "W*K too large for the LDS budget"));
   env->c = c;
   env->s = s;
+  {
+    DevEnv hd{c, s};
+    if (hipMalloc(&env->dev, sizeof(DevEnv)) != hipSuccess ||
+        hipMemcpy(env->dev, &hd, sizeof(DevEnv), hipMemcpyHostToDevice) != hipSuccess)
+      return fail(set_err(-2, "device descriptor upload failed"));
+  }
   *out = env;
   return 0;
 }
@@ -339,6 +357,7 @@ void msc_env_destroy(msc_env* env) {
   if (env->tables) (void)hipFree(env->tables);
   if (env->arena) (void)hipFree(env->arena);
   if (env->scratch) (void)hipFree(env->scratch);
+  if (env->dev) (void)hipFree(env->dev);
   delete env;
 }
 
@@ -359,7 +378,7 @@ int msc_env_reset(msc_env* env, const uint8_t* mask, const uint32_t* new_root_se
                   msc_stream_t stream) {
   if (!env) return set_err(-1, "null env");
   env->demand_ready = false;  // a reset re-seeds the demand streams
-  HIP_TRY(launch_reset(env->c, env->s, mask, new_root_seeds, flags, obs, (hipStream_t)stream));
+  HIP_TRY(launch_reset(env->c, env->dev, mask, new_root_seeds, flags, obs, (hipStream_t)stream));
   return 0;
 }
 
@@ -392,7 +411,7 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
     for (auto& q : z)
       if (q.p) HIP_TRY(hipMemsetAsync(q.p, 0, q.n, st));
   }
-  HIP_TRY(launch_step(c, env->s, io, !env->demand_ready, st));
+  HIP_TRY(launch_step(c, env->dev, io, !env->demand_ready, st));
   env->demand_ready = false;
   return 0;
 }
@@ -400,7 +419,7 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
 int msc_env_generate_demand(msc_env* env, msc_stream_t stream) {
   if (!env) return set_err(-1, "null env");
   if (env->c.demand_type != MSC_DEMAND_POISSON) return 0;
-  HIP_TRY(launch_demand(env->c, env->s, (hipStream_t)stream));
+  HIP_TRY(launch_demand(env->c, env->dev, (hipStream_t)stream));
   env->demand_ready = true;
   return 0;
 }

@@ -12,6 +12,15 @@
 
 namespace msc {
 
+// Device compilation sees every buffer pointer of the descriptor as a GLOBAL (addrspace 1) pointer:
+// loads through pointers fetched from the device-resident DevEnv are otherwise generic flat_*
+// instructions, which also count against lgkmcnt (so every LDS wait would wait for them too).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MSC_G __attribute__((address_space(1)))
+#else
+#define MSC_G
+#endif
+
 constexpr int BS = 64;          // threads per block of the env kernels (one wave: one env per lane)
 constexpr int MAX_RING = 64;    // pending-order ring slots (max actual lead time + 1)
 
@@ -19,68 +28,92 @@ struct EnvConst {
   int32_t W, K, R, T, Lmax, RING, F, L, order_cap;
   int32_t action_type, lead_type, dev_per_sku, lost_type, scope, norm, wid, num_eval, max_wh;
   int32_t demand_type, init_type, init_min, init_max, hold_per_sku, pen_per_sku, tr_rows;
+  int32_t cost_lds;     // 1: step kernel stages the [R][W] outbound cost tables in LDS
+  int32_t dem_lds;      // 1: demand kernel stages the Poisson rate tables in LDS
+  int32_t ablate;       // timing-only phase ablation bits (MSC_ABLATE env var); 0 in production
+  int32_t demand_impl;  // 0 = flat state machine (default), 1 = nested loops (MSC_DEMAND_IMPL=nested, A/B only)
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;
-  const double* act_param;   // [K]
-  const int32_t* init_vals;  // [W*K]
-  const double* hold;        // [K]
-  const double* pen;         // [K]
-  const double* skw;         // [K]
-  const double* ofT;         // [R][W] outbound fixed (transposed: one region's row is contiguous)
-  const double* ovT;         // [R][W] outbound variable
-  const double* inF;         // [W*K]
-  const double* inV;         // [W*K]
-  const double* enlam_o;     // [R]   exp(-lambda_orders) from the host libm
-  const double* p_sku;       // [R]
-  const double* enlam_q;     // [R*K] exp(-lambda_quantity)
-  const int32_t* elt;        // [W*K] expected lead times
-  const int32_t* maxdev;     // [K] or [1]
-  const uint32_t* home_mask; // [R] bit w set <=> region r is warehouse w's home region
-  const int32_t* closest;    // [R] closest warehouse of each region
-  const float* obs_mean;     // [F]
-  const float* obs_std;      // [F]
-  const int64_t* tr_off;     // [tr_rows + 1]
+  const MSC_G double* act_param;   // [K]
+  const MSC_G int32_t* init_vals;  // [W*K]
+  const MSC_G double* hold;        // [K]
+  const MSC_G double* pen;         // [K]
+  const MSC_G double* skw;         // [K]
+  const MSC_G double* ofT;         // [R][W] outbound fixed (transposed: one region's row is contiguous)
+  const MSC_G double* ovT;         // [R][W] outbound variable
+  const MSC_G double* inF;         // [W*K]
+  const MSC_G double* inV;         // [W*K]
+  const MSC_G double* enlam_o;     // [R]   exp(-lambda_orders) from the host libm
+  const MSC_G double* p_sku;       // [R]
+  const MSC_G double* enlam_q;     // [R*K] exp(-lambda_quantity)
+  const MSC_G int32_t* elt;        // [W*K] expected lead times
+  const MSC_G int32_t* maxdev;     // [K] or [1]
+  const MSC_G uint32_t* home_mask; // [R] bit w set <=> region r is warehouse w's home region
+  const MSC_G int32_t* closest;    // [R] closest warehouse of each region
+  const MSC_G float* obs_mean;     // [F]
+  const MSC_G float* obs_std;      // [F]
+  const MSC_G int64_t* tr_off;     // [tr_rows + 1]
   const uint4* tr_rec;       // [n_trace_orders][NV] packed order records
 };
 
 struct EnvState {
-  int32_t* inv;        // [WK][E]
-  int32_t* ring_q;     // [WK][RING][E] pending quantity by order time mod RING (0 = empty)
-  uint8_t* ring_l;     // [WK][RING][E] actual lead time of that order (stochastic lead only)
-  int32_t* hist;       // [5][WK][E]    incoming home demand of step tau at slot tau % 5
-  int32_t* inc;        // [WK][E]       incoming home demand of the last step
-  float* fc;           // [WK][E]       EMA demand forecast (f32, multi_env.py:789-793)
-  uint64_t* rng;       // [2][4][E]     {demand, lead} x {s_hi, s_lo, i_hi, i_lo}
-  uint32_t* rbuf;      // [2][2][E]     {demand, lead} x {has32, u32}
-  int32_t* t;          // [E] timestep
-  int32_t* counter;    // [E] SeedManager._episode_counter
-  uint32_t* orig_root; // [E] SeedManager._original_root_seed
-  uint32_t* root;      // [E] SeedManager.root_seed
-  int32_t* emp_start;  // [E] EmpiricalDemandSampler window start row (-1: not drawn)
+  MSC_G int32_t* inv;        // [WK][E]
+  MSC_G int32_t* ring_q;     // [WK][RING][E] pending quantity by order time mod RING (0 = empty)
+  MSC_G uint8_t* ring_l;     // [WK][RING][E] actual lead time of that order (stochastic lead only)
+  MSC_G int32_t* hist;       // [5][WK][E]    incoming home demand of step tau at slot tau % 5
+  MSC_G int32_t* inc;        // [WK][E]       incoming home demand of the last step
+  MSC_G float* fc;           // [WK][E]       EMA demand forecast (f32, multi_env.py:789-793)
+  MSC_G uint64_t* rng;       // [2][4][E]     {demand, lead} x {s_hi, s_lo, i_hi, i_lo}
+  MSC_G uint32_t* rbuf;      // [2][2][E]     {demand, lead} x {has32, u32}
+  MSC_G int32_t* t;          // [E] timestep
+  MSC_G int32_t* counter;    // [E] SeedManager._episode_counter
+  MSC_G uint32_t* orig_root; // [E] SeedManager._original_root_seed
+  MSC_G uint32_t* root;      // [E] SeedManager.root_seed
+  MSC_G int32_t* emp_start;  // [E] EmpiricalDemandSampler window start row (-1: not drawn)
   uint4* orders;       // [order_cap][E][NV] per-step order records (Poisson sampler output)
-  int32_t* n_orders;   // [E]
-  uint32_t* err;       // [1] device error bits
+  MSC_G int32_t* n_orders;   // [E]
+  MSC_G uint32_t* err;       // [1] device error bits
 };
 
 struct StepIO {
-  const float* actions;  // [E][W][K]
-  float* obs;            // [E][W][L]
-  float* rew;            // [E][W]
-  double* rew64;         // [E][W] or null
-  uint8_t* trunc;        // [E]
-  float* final_obs;      // [E][W][L] or null
+  const MSC_G float* actions;  // [E][W][K]
+  MSC_G float* obs;            // [E][W][L]
+  MSC_G float* rew;            // [E][W]
+  MSC_G double* rew64;         // [E][W] or null
+  MSC_G uint8_t* trunc;        // [E]
+  MSC_G float* final_obs;      // [E][W][L] or null
   msc_step_info info;    // device pointers or nulls
   int32_t has_info;
 };
 
 constexpr uint32_t ERR_ORDER_OVERFLOW = 1u;
 
+// int32 words of the step kernel's per-lane LDS arrays (inventory, shipped-to-region,
+// shipped-total, shipped-home: 4*W*K; pipeline buckets: Lmax*K), rounded to 16 B.
+__host__ __device__ inline int step_lds_ints(const EnvConst& c) {
+  const int n = (4 * c.W * c.K + c.Lmax * c.K) * BS;
+  return (n + 3) & ~3;
+}
+// total dynamic LDS of the step kernel, with or without the shared outbound cost table
+inline size_t step_lds_bytes_for(const EnvConst& c, bool cost_table) {
+  return (size_t)step_lds_ints(c) * 4 + (size_t)3 * c.W * BS * sizeof(double) +
+         (cost_table ? (size_t)2 * c.R * c.W * sizeof(double) + (size_t)2 * c.R * sizeof(int32_t) : 0);
+}
+constexpr size_t LDS_BUDGET = 160 * 1024;
+
 // launchers (env_kernels.hip)
-hipError_t launch_reset(const EnvConst& c, const EnvState& s, const uint8_t* mask, const uint32_t* new_roots,
+// The descriptor + state pointers live in device memory and kernels take a pointer to them:
+// fields are then scalar-cache loads, and no address-taken kernel argument is copied to scratch.
+struct DevEnv {
+  EnvConst c;
+  EnvState s;
+};
+
+hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask, const uint32_t* new_roots,
                         int32_t flags, float* obs, hipStream_t st);
-hipError_t launch_step(const EnvConst& c, const EnvState& s, const StepIO& io, bool gen_demand, hipStream_t st);
-hipError_t launch_demand(const EnvConst& c, const EnvState& s, hipStream_t st);
+hipError_t launch_step(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen_demand, hipStream_t st);
+hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st);
 hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hipStream_t st);
 size_t step_lds_bytes(const EnvConst& c);
 int order_record_vec4(int K);

@@ -21,6 +21,25 @@
 
 namespace msc {
 
+// Explicit global address space for hot buffers: pointers loaded from the device-resident DevEnv
+// are generic, and generic (flat_*) loads also count against lgkmcnt, so any LDS wait would also
+// wait for them and defeat software prefetching.
+#define MSC_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ MSC_GLOBAL T* gp(T* p) {
+  return (MSC_GLOBAL T*)p;
+}
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // uint4 as a native vector type
+__device__ __forceinline__ uint4 gload4(const MSC_GLOBAL uint4* p, int64_t i) {
+  const v4u v = reinterpret_cast<const MSC_GLOBAL v4u*>(p)[i];
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gstore4(MSC_GLOBAL uint4* p, int64_t i, uint4 x) {
+  v4u v;
+  v.x = x.x; v.y = x.y; v.z = x.z; v.w = x.w;
+  reinterpret_cast<MSC_GLOBAL v4u*>(p)[i] = v;
+}
+
 // ------------------------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------------------------
@@ -98,7 +117,8 @@ __device__ __forceinline__ float np_sum_f32(const float (&a)[K]) {
 // reset (multi_env.py:192-251, SeedManager.advance_episode / update_root_seed)
 // ------------------------------------------------------------------------------------------
 template <int K>
-__device__ void reset_env(const EnvConst& c, const EnvState& s, int64_t e, int32_t flags, const uint32_t* new_root) {
+__device__ __noinline__ void reset_env(const EnvConst& c, const EnvState& s, int64_t e, int32_t flags,
+                                       const uint32_t* new_root) {
   const int64_t E = c.E;
   const int WK = c.W * K;
   uint32_t root;
@@ -143,9 +163,10 @@ __device__ void reset_env(const EnvConst& c, const EnvState& s, int64_t e, int32
 //   n_hist: entries in the demand-history deque (0 at reset)
 //   shh/sht: per-lane LDS shipped-home / shipped-total of this step (null at reset)
 // ------------------------------------------------------------------------------------------
+//   pipe   : per-lane LDS scratch of Lmax*K ints ([l*K + sku] * BS), the pipeline buckets
 template <int K>
-__device__ void build_obs(const EnvConst& c, const EnvState& s, int64_t e, int t_now, int n_hist,
-                          const int32_t* shh, const int32_t* sht, float* out) {
+__device__ __noinline__ void build_obs(const EnvConst& c, const EnvState& s, int64_t e, int t_now, int n_hist,
+                                       const int32_t* shh, const int32_t* sht, int32_t* pipe, float* out) {
   const int64_t E = c.E;
   const int W = c.W, RING = c.RING, Lmax = c.Lmax;
   const uint32_t f = c.flags;
@@ -178,30 +199,28 @@ __device__ void build_obs(const EnvConst& c, const EnvState& s, int64_t e, int t
       rm[sk] = n_hist > 0 ? (float)hs / (float)n_hist : 0.0f;
       pend_sum[sk] = 0;
     }
-    // pipeline bucket of each pending order: expected arrival - t_now, overdue -> slot 0
-    auto pipe_at = [&](int l, int sk) -> int {
+    // pipeline bucket of each pending order (one pass over the ring): expected arrival - t_now,
+    // overdue orders into slot 0 (_compute_pipeline, multi_env.py:956-966)
+    for (int l = 0; l < Lmax * K; l++) pipe[l * BS] = 0;
+    int pend_total = 0;
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
       const int i = w * K + sk;
       const int elt = c.elt[i];
-      int acc = 0;
+      const int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
       for (int jr = 0; jr < RING; jr++) {
-        int q = s.ring_q[(i * RING + jr) * E + e];
+        const int q = rq[jr * E];
         if (q == 0) continue;
         int age = (t_now - jr) % RING;
         if (age < 0) age += RING;
         int slot = elt - age;
-        if (slot < 1) slot = 1;
-        if (slot - 1 == l) acc += q;
+        slot = slot < 1 ? 1 : slot;
+        pipe[((slot - 1) * K + sk) * BS] += q;
+        pend_sum[sk] += q;
       }
-      return acc;
-    };
-    int pend_total = 0;
-    for (int l = 0; l < Lmax; l++)
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) {
-        int v = pipe_at(l, sk);
-        pend_total += v;
-        pend_sum[sk] += v;
-      }
+      pend_total += pend_sum[sk];
+    }
+    auto pipe_at = [&](int l, int sk) -> int { return pipe[(l * K + sk) * BS]; };
     double inv_total = 0.0, shipped_total = 0.0, sa_total = 0.0;
     float dh_total = 0.0f;
 #pragma unroll
@@ -311,19 +330,277 @@ __device__ void build_obs(const EnvConst& c, const EnvState& s, int64_t e, int t
 // kernels
 // ------------------------------------------------------------------------------------------
 template <int K>
-__global__ __launch_bounds__(BS) void reset_kernel(EnvConst c, EnvState s, const uint8_t* mask,
+__global__ __launch_bounds__(BS) void reset_kernel(const DevEnv* __restrict__ dp, const uint8_t* mask,
                                                    const uint32_t* new_roots, int32_t flags, float* obs) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  extern __shared__ __attribute__((aligned(16))) int32_t lds[];  // [Lmax*K][BS] pipeline scratch
   const int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x;
   if (e >= c.E) return;
   if (mask && !mask[e]) return;
   reset_env<K>(c, s, e, flags, new_roots ? new_roots + e : nullptr);
-  if (obs) build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, obs + e * c.W * c.L);
+  if (obs) build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, lds + threadIdx.x, obs + e * c.W * c.L);
 }
 
-// PoissonDemandSampler.sample (demand_sampler.py:105-163): per region n ~ Poisson(lambda_o);
-// per order K Bernoulli(p) SKU draws then max(1, Poisson(lambda_q)) for the selected SKUs.
+// PoissonDemandSampler.sample (demand_sampler.py:105-163), production version: a flat per-lane
+// parser whose every iteration draws ONE uniform per active lane and then settles the zero-draw
+// transitions in a single branch-free pass. The pass is complete because the reference schema
+// requires every Poisson rate to be strictly positive (PositiveFloat, src/config/schema.py:191),
+// so each chain qty-done -> emit -> next order / next region ends at a state that draws.
+// The thresholds a lane may need in the NEXT pass (its next SKU's exp(-lambda_q), the next
+// region's exp(-lambda_o) and p) are prefetched from LDS at the end of each pass, so the LDS
+// latency hides under the following PCG64 draw. No branch except the order-record store.
+constexpr int PS_MASK = 0, PS_ORD = 1, PS_QTY = 2, PS_DONE = 3;
+
+template <int K, bool LDS_TAB>
+__global__ __launch_bounds__(BS) void demand_flat_kernel(const DevEnv* __restrict__ dp) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  const int R = c.R;
+  extern __shared__ __attribute__((aligned(16))) double tlds[];
+  const double* To = c.enlam_o;  // [R]
+  const double* Tp = c.p_sku;    // [R]
+  const double* Tq = c.enlam_q;  // [R*K]
+  if constexpr (LDS_TAB) {
+    double* lo = tlds;
+    double* lp = tlds + R;
+    double* lq = tlds + 2 * R;
+    for (int i = threadIdx.x; i < R; i += BS) {
+      lo[i] = c.enlam_o[i];
+      lp[i] = c.p_sku[i];
+    }
+    for (int i = threadIdx.x; i < R * K; i += BS) lq[i] = c.enlam_q[i];
+    __syncthreads();
+    To = lo;
+    Tp = lp;
+    Tq = lq;
+  }
+  const int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x;
+  if (e >= c.E) return;
+  const int64_t E = c.E;
+  constexpr int NV = Rec<K>::NV;
+  constexpr int NW = 2 * NV;
+  Pcg64 rg = load_rng(s, 0, e, E);
+  int st = PS_ORD, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0;
+  unsigned mask = 0;
+  double prod = 1.0, thr = To[0], p = Tp[0];
+  uint64_t rec[NW];
+#pragma unroll
+  for (int j = 0; j < NW; j++) rec[j] = 0;
+  // prefetched for the next pass
+  double pre_o = To[R > 1 ? 1 : 0], pre_p = Tp[R > 1 ? 1 : 0], pre_q = Tq[0];
+  MSC_GLOBAL uint4* out = gp(s.orders + e);
+  const int cap = c.order_cap;
+  while (st != PS_DONE) {
+    const double U = pcg_double(rg);
+    // ---- consume the draw
+    const bool in_mask = st == PS_MASK;
+    const double prod_u = prod * U;
+    const bool cont = prod_u > thr;
+    const unsigned mask_u = mask | ((U < p) ? (1u << k) : 0u);
+    const bool ev_maskdone = in_mask && (k + 1 == K);
+    const bool ev_done = !in_mask && !cont;
+    const bool ev_region = ev_done && st == PS_ORD;
+    const bool ev_qty = ev_done && st == PS_QTY;
+    mask = in_mask ? mask_u : mask;
+    k = in_mask ? k + 1 : k;
+    prod = in_mask ? prod : prod_u;
+    x = (!in_mask && cont) ? x + 1 : x;
+    // ---- settle: quantity of the current SKU, then next SKU or emit, then next order/region
+    {
+      const uint64_t v = (uint64_t)(x > 1 ? x : 1);
+      const int sh = 16 * (1 + sq);
+#pragma unroll
+      for (int j = 0; j < NW; j++) rec[j] |= (ev_qty && (sh >> 6) == j) ? v << (sh & 63) : 0;
+    }
+    mask = ev_qty ? (mask & (mask - 1u)) : mask;
+    const bool next_sku = ev_maskdone || ev_qty;
+    const bool start_q = next_sku && mask != 0;
+    const bool emit = next_sku && mask == 0;
+    sq = start_q ? __builtin_ctz(mask) : sq;
+    left = ev_region ? x : left;
+    if (emit && n < cap) {
+#pragma unroll
+      for (int j = 0; j < NV; j++)
+        gstore4(out, ((int64_t)n * NV + j) * E,
+                make_uint4((uint32_t)rec[2 * j], (uint32_t)(rec[2 * j] >> 32), (uint32_t)rec[2 * j + 1],
+                           (uint32_t)(rec[2 * j + 1] >> 32)));
+    }
+    n += emit ? 1 : 0;
+    left -= emit ? 1 : 0;
+    const bool next_order = emit || ev_region;
+    const bool start_order = next_order && left > 0;
+    const bool next_region = next_order && left == 0;
+    const bool done = next_region && r + 1 == R;
+    const bool start_region = next_region && !done;
+    r = start_region ? r + 1 : r;
+#pragma unroll
+    for (int j = 0; j < NW; j++) rec[j] = start_order ? (j == 0 ? (uint64_t)r : 0) : rec[j];
+    mask = start_order ? 0u : mask;
+    k = start_order ? 0 : k;
+    thr = start_q ? pre_q : (start_region ? pre_o : thr);
+    p = start_region ? pre_p : p;
+    prod = (start_q || start_region) ? 1.0 : prod;
+    x = (start_q || start_region) ? 0 : x;
+    st = done ? PS_DONE : start_region ? PS_ORD : start_order ? PS_MASK : start_q ? PS_QTY : st;
+    // ---- prefetch what the next pass may need
+    const unsigned nm = mask & (mask - 1u);
+    const int cand = st == PS_QTY ? (nm ? __builtin_ctz(nm) : 0) : (mask ? __builtin_ctz(mask) : K - 1);
+    const int rn = r + 1 < R ? r + 1 : r;
+    pre_q = Tq[r * K + cand];
+    pre_o = To[rn];
+    pre_p = Tp[rn];
+  }
+  store_rng(s, 0, e, E, rg);
+  if (n > cap) {
+    atomicOr(s.err, ERR_ORDER_OVERFLOW);
+    n = cap;
+  }
+  s.n_orders[e] = n;
+}
+
+// Variant with branchy settling (kept for A/B measurement: MSC_DEMAND_IMPL=flat_branchy).
+//
+// The reference's draw sequence per step is: for each region, Poisson(lambda_o) (multiplication
+// method: uniforms until the running product drops to exp(-lambda)); per order K uniforms for the
+// Bernoulli SKU mask; per selected SKU (ascending) max(1, Poisson(lambda_q)). Written as nested
+// loops, the 64 lanes of a wave re-converge at every region/order/SKU boundary and wait for the
+// slowest lane each time (~7x wasted issue). Here every loop iteration draws exactly one uniform
+// per active lane and advances that lane's own parser; the zero-draw transitions (region done,
+// empty order, order emitted) are settled per lane before the next draw. A wave therefore runs
+// for max-over-lanes of the TOTAL draws per step (~6.7k at 8x64x5, within ~15% of the mean).
+enum : int { ST_MASK = 0, ST_POIS = 1, ST_REGION = 2, ST_ORDERS = 3, ST_MASKDONE = 4, ST_QSTART = 5, ST_QNEXT = 6, ST_DONE = 7 };
+
 template <int K>
-__global__ __launch_bounds__(BS) void demand_poisson_kernel(EnvConst c, EnvState s) {
+__global__ __launch_bounds__(BS) void demand_poisson_kernel(const DevEnv* __restrict__ dp) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  // rate tables in LDS: each lane gathers its own region's thresholds on every settle
+  extern __shared__ __attribute__((aligned(16))) double dlds[];
+  double* Lo = dlds;            // [R]   exp(-lambda_orders)
+  double* Lp = dlds + c.R;      // [R]   probability_skus
+  double* Lq = dlds + 2 * c.R;  // [R*K] exp(-lambda_quantity)
+  const bool tl = c.dem_lds != 0;
+  if (tl) {
+    for (int i = threadIdx.x; i < c.R; i += BS) {
+      Lo[i] = c.enlam_o[i];
+      Lp[i] = c.p_sku[i];
+    }
+    for (int i = threadIdx.x; i < c.R * K; i += BS) Lq[i] = c.enlam_q[i];
+    __syncthreads();
+  }
+  const int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x;
+  if (e >= c.E) return;
+  const int64_t E = c.E;
+  const int R = c.R;
+  constexpr int NV = Rec<K>::NV;
+  constexpr int NW = 2 * NV;  // 64-bit words of a record
+  Pcg64 rg = load_rng(s, 0, e, E);
+  int st = ST_REGION, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0;
+  bool isq = false;
+  unsigned mask = 0;
+  double prod = 1.0, thr = 0.0, p = 0.0;
+  uint64_t rec[NW];
+#pragma unroll
+  for (int j = 0; j < NW; j++) rec[j] = 0;
+  uint4* out = s.orders + e;
+  for (;;) {
+    // Settle the transitions that consume no draw, in their natural order, as one straight-line
+    // pass (a chain qty-done -> emit -> next order / next region completes in one pass; only a
+    // zero-rate quantity or region repeats it).
+    while (st >= ST_REGION && st != ST_DONE) {
+      if (st == ST_MASKDONE) {
+        if (mask) {
+          sq = __builtin_ctz(mask);
+          st = ST_QSTART;
+        } else {
+          st = ST_QNEXT;
+        }
+      }
+      if (st == ST_QSTART) {
+        thr = tl ? Lq[r * K + sq] : c.enlam_q[r * K + sq];
+        if (thr >= 1.0) {  // lambda == 0: Poisson -> 0 without a draw, quantity max(1, 0)
+          const int sh = 16 * (1 + sq);
+#pragma unroll
+          for (int j = 0; j < NW; j++) rec[j] |= (sh >> 6) == j ? (uint64_t)1 << (sh & 63) : 0;
+          mask &= mask - 1u;
+          st = mask ? ST_MASKDONE : ST_QNEXT;
+        } else {
+          prod = 1.0; x = 0; isq = true; st = ST_POIS;
+        }
+      }
+      if (st == ST_QNEXT) {  // every selected SKU drawn: emit the order
+        if (n < c.order_cap) {
+          uint4* dst = out + (int64_t)n * NV * E;
+#pragma unroll
+          for (int j = 0; j < NV; j++)
+            dst[j * E] = make_uint4((uint32_t)rec[2 * j], (uint32_t)(rec[2 * j] >> 32), (uint32_t)rec[2 * j + 1],
+                                    (uint32_t)(rec[2 * j + 1] >> 32));
+        }
+        n++;
+        left--;
+        st = ST_ORDERS;
+      }
+      if (st == ST_ORDERS) {
+        if (left == 0) {
+          r++;
+          st = ST_REGION;
+        } else {
+          mask = 0; k = 0; st = ST_MASK;
+#pragma unroll
+          for (int j = 0; j < NW; j++) rec[j] = 0;
+          rec[0] = (uint64_t)r;
+        }
+      }
+      if (st == ST_REGION) {
+        if (r == R) {
+          st = ST_DONE;
+        } else {
+          thr = tl ? Lo[r] : c.enlam_o[r];
+          p = tl ? Lp[r] : c.p_sku[r];
+          if (thr >= 1.0) {  // lambda == 0: no orders, no draw
+            left = 0; st = ST_ORDERS;
+          } else {
+            prod = 1.0; x = 0; isq = false; st = ST_POIS;
+          }
+        }
+      }
+    }
+    if (st == ST_DONE) break;
+    const double U = pcg_double(rg);
+    if (st == ST_MASK) {
+      mask |= (U < p) ? (1u << k) : 0u;
+      if (++k == K) st = ST_MASKDONE;
+    } else {
+      prod *= U;
+      if (prod > thr) {
+        x++;
+      } else if (!isq) {
+        left = x;
+        st = ST_ORDERS;
+      } else {
+        const uint64_t v = (uint64_t)(x > 1 ? x : 1);
+        const int sh = 16 * (1 + sq);
+#pragma unroll
+        for (int j = 0; j < NW; j++) rec[j] |= (sh >> 6) == j ? v << (sh & 63) : 0;
+        mask &= mask - 1u;
+        st = mask ? ST_MASKDONE : ST_QNEXT;
+      }
+    }
+  }
+  store_rng(s, 0, e, E, rg);
+  if (n > c.order_cap) {
+    atomicOr(s.err, ERR_ORDER_OVERFLOW);
+    n = c.order_cap;
+  }
+  s.n_orders[e] = n;
+}
+
+// Reference-shaped nested-loop version (kept for A/B measurement; not launched).
+template <int K>
+__global__ __launch_bounds__(BS) void demand_poisson_nested_kernel(const DevEnv* __restrict__ dp) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
   const int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x;
   if (e >= c.E) return;
   const int64_t E = c.E;
@@ -378,22 +655,52 @@ __device__ __forceinline__ void sort_costs(double (&c)[WM], int (&ix)[WM]) {
     for (int a = round & 1; a + 1 < WM; a += 2) cas(c[a], ix[a], c[a + 1], ix[a + 1]);
 }
 
-template <int K, int WM>
-__global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO io) {
+template <int K, int WM, bool TAB_LDS>
+__global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
   extern __shared__ __attribute__((aligned(16))) int32_t lds[];
   const int lane = threadIdx.x;
   const int64_t e = (int64_t)blockIdx.x * BS + lane;
-  if (e >= c.E) return;
   const int64_t E = c.E;
   const int W = c.W, WK = W * K, R = c.R, RING = c.RING;
+  // LDS: per-lane [field][idx][lane] arrays, then the block-shared outbound cost table
+  const int ni = step_lds_ints(c);
   int32_t* Linv = lds + lane;                 // [WK]  inventory
   int32_t* Lqsr = lds + 1 * WK * BS + lane;   // [WK]  shipped to the current region
   int32_t* Lsht = lds + 2 * WK * BS + lane;   // [WK]  shipped in total this step
   int32_t* Lshh = lds + 3 * WK * BS + lane;   // [WK]  shipped to the home region
-  double* Lpen = reinterpret_cast<double*>(lds + 4 * WK * BS) + lane;  // [W] penalty cost
-  double* Lout = Lpen + W * BS;                                        // [W] outbound cost
-  double* Linb = Lout + W * BS;                                        // [W] inbound cost
-  const msc_step_info& info = io.info;
+  int32_t* Lpipe = lds + 4 * WK * BS + lane;  // [Lmax*K] pipeline buckets (observations)
+  double* Lpen = reinterpret_cast<double*>(lds + ni) + lane;  // [W] penalty cost
+  double* Lout = Lpen + W * BS;                                // [W] outbound cost
+  double* Linb = Lout + W * BS;                                // [W] inbound cost
+  // block-shared per-region tables: [2][R][W] f64 outbound costs, [R] closest, [R] home mask
+  const double* OFt = c.ofT;
+  const double* OVt = c.ovT;
+  const int32_t* CLt = c.closest;
+  const uint32_t* HMt = c.home_mask;
+  if constexpr (TAB_LDS) {
+    double* Tcost = reinterpret_cast<double*>(lds + ni) + 3 * W * BS;
+    int32_t* Tcl = reinterpret_cast<int32_t*>(Tcost + 2 * R * W);
+    uint32_t* Thm = reinterpret_cast<uint32_t*>(Tcl + R);
+    for (int i = lane; i < R * W; i += BS) {
+      Tcost[i] = c.ofT[i];
+      Tcost[R * W + i] = c.ovT[i];
+    }
+    for (int i = lane; i < R; i += BS) {
+      Tcl[i] = c.closest[i];
+      Thm[i] = c.home_mask[i];
+    }
+    __syncthreads();
+    OFt = Tcost;
+    OVt = Tcost + R * W;
+    CLt = Tcl;
+    HMt = Thm;
+  }
+  if (e >= c.E) return;
+  auto OF = [&](int r, int w) -> double { return OFt[r * W + w]; };
+  auto OV = [&](int r, int w) -> double { return OVt[r * W + w]; };
+  const msc_step_info info = io.info;
   const bool dbg = io.has_info != 0;
 
   const int t = s.t[e];
@@ -489,7 +796,7 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
     for (int i = 0; i < WK; i++) Lqsr[i * BS] = 0;
 
   // ---- phase B: greedy allocation (demand_allocator.py:118-217) + per-region epilogue ------
-  const uint4* src;
+  const MSC_GLOBAL uint4* src;
   int64_t stride;
   int n_orders;
   if (c.demand_type == MSC_DEMAND_EMPIRICAL) {  // demand_sampler.py:227-241
@@ -503,11 +810,11 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
     const int64_t row = st0 + (t % c.T);
     const int64_t off = c.tr_off[row];
     n_orders = (int)(c.tr_off[row + 1] - off);
-    src = c.tr_rec + off * Rec<K>::NV;
+    src = gp(c.tr_rec + off * Rec<K>::NV);
     stride = 1;
   } else {
     n_orders = s.n_orders[e];
-    src = s.orders + e;
+    src = gp(s.orders + e);
     stride = E;
   }
   if (dbg && info.n_orders) info.n_orders[e] = n_orders;
@@ -528,7 +835,7 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
       for (int sk = 0; sk < K; sk++)
         upen += c.pen_per_sku ? (double)u[sk] * c.pen[sk] : ((double)u[sk] * c.skw[sk]) * c.pen_scalar;
       if (c.lost_type == MSC_LOST_CLOSEST) {
-        const int w0 = c.closest[r];
+        const int w0 = CLt[r];
         Lpen[w0 * BS] += upen;
         if (dbg && info.lost_sales)
 #pragma unroll
@@ -559,7 +866,7 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
             }
           }
         } else {
-          const int w0 = c.closest[r];
+          const int w0 = CLt[r];
           Lpen[w0 * BS] += upen;
           if (dbg && info.lost_sales)
 #pragma unroll
@@ -572,7 +879,7 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
         double lg[WM], mx = -INFINITY, se = 0.0;
 #pragma unroll
         for (int w = 0; w < WM; w++) {
-          lg[w] = w < W ? -(c.ofT[r * W + w] * (double)lost_cnt + c.ovT[r * W + w] * lw) / c.alpha : -INFINITY;
+          lg[w] = w < W ? -(OF(r, w) * (double)lost_cnt + OV(r, w) * lw) / c.alpha : -INFINITY;
           mx = lg[w] > mx ? lg[w] : mx;
         }
 #pragma unroll
@@ -593,7 +900,7 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
       }
     }
     // home-region features: incoming demand and units shipped home (multi_env.py:767-773)
-    unsigned hm = c.home_mask[r];
+    unsigned hm = HMt[r];
     while (hm) {
       const int w = __builtin_ctz(hm);
       hm &= hm - 1u;
@@ -619,9 +926,50 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
   };
 
   const int maxwh = c.max_wh;
-  for (int oi = 0; oi < n_orders; oi++) {
-    int r, d[K];
-    load_rec<K>(src + oi * rec_step, stride, r, d);
+  // nz[s]: bitmask of warehouses holding stock of SKU s, kept exact through every fill. The
+  // greedy loop only ever ships from a warehouse that has stock of a still-needed SKU, so the
+  // ranked visit of demand_allocator.py:180-203 is equivalent to repeated argmin over that
+  // candidate set (lowest index on cost ties = a stable argsort), and an order whose SKUs are
+  // out of stock everywhere is lost without ranking anything.
+  unsigned nz[K];
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) nz[sk] = 0u;
+  for (int w = 0; w < W; w++)
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) nz[sk] |= Linv[(w * K + sk) * BS] > 0 ? (1u << w) : 0u;
+  if (c.ablate & 2) n_orders = 0;  // timing-only ablation (MSC_ABLATE), never set in production
+  // order records are software-pipelined PF ahead through a register ring (raw uint4 words, so
+  // the loads stay in flight); the loop runs once past the last order as a sentinel so the region
+  // epilogue has a single call site
+  constexpr int NVR = Rec<K>::NV;
+  constexpr int PF = 4;
+  uint4 ring[PF][NVR];
+#pragma unroll
+  for (int q = 0; q < PF; q++)
+#pragma unroll
+    for (int j = 0; j < NVR; j++) ring[q][j] = (q < n_orders) ? gload4(src, q * rec_step + j * stride) : make_uint4(0, 0, 0, 0);
+  for (int oi = 0; oi <= n_orders; oi++) {
+    int r = -1;
+    int d[K];
+    {
+      union {
+        uint4 v[NVR];
+        uint16_t h[8 * NVR];
+      } u;
+#pragma unroll
+      for (int j = 0; j < NVR; j++) u.v[j] = ring[0][j];
+      if (oi < n_orders) r = u.h[0];
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) d[sk] = u.h[1 + sk];
+    }
+#pragma unroll
+    for (int q = 0; q + 1 < PF; q++)
+#pragma unroll
+      for (int j = 0; j < NVR; j++) ring[q][j] = ring[q + 1][j];
+    if (oi + PF < n_orders) {
+#pragma unroll
+      for (int j = 0; j < NVR; j++) ring[PF - 1][j] = gload4(src, (oi + PF) * rec_step + j * stride);
+    }
     if (r != cur) {
       if (cur >= 0) finalize(cur);
       cur = r;
@@ -630,6 +978,7 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
 #pragma unroll
       for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
     }
+    if (oi == n_orders) break;
     bool any_d = false;
     double tw = 0.0;
 #pragma unroll
@@ -639,57 +988,69 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
       tw += (double)d[sk] * c.skw[sk];
     }
     if (!any_d) continue;  // an empty order ships nothing and is never lost
-    double cst[WM];
-    int ix[WM];
-#pragma unroll
-    for (int w = 0; w < WM; w++) {
-      cst[w] = w < W ? c.ofT[r * W + w] + c.ovT[r * W + w] * tw : INFINITY;
-      ix[w] = w;
-    }
-    sort_costs<WM>(cst, ix);
     int rem[K];
+    unsigned cand = 0u;
 #pragma unroll
-    for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
-    int used = 0;
+    for (int sk = 0; sk < K; sk++) {
+      rem[sk] = d[sk];
+      cand |= d[sk] > 0 ? nz[sk] : 0u;
+    }
+    if (cand) {
+      double cst[WM];  // cost = fixed + variable * order weight (demand_allocator.py:168-172)
 #pragma unroll
-    for (int k = 0; k < WM; k++) {
-      if (k >= W || used >= maxwh) break;
-      const int w = ix[k];
-      int fl[K];
-      bool any = false;
+      for (int w = 0; w < WM; w++) cst[w] = (w < W && (cand >> w & 1u)) ? OF(r, w) + OV(r, w) * tw : INFINITY;
+      int used = 0;
+      while (cand && used < maxwh) {
+        int w = 0;
+        double bc = INFINITY;
 #pragma unroll
-      for (int sk = 0; sk < K; sk++) {
-        const int iv = Linv[(w * K + sk) * BS];
-        fl[sk] = rem[sk] < iv ? rem[sk] : iv;
-        any |= fl[sk] > 0;
-      }
-      if (!any) continue;
-      double fw = 0.0;
-      int fsum = 0;
-      bool done = true;
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) {
-        const int idx = (w * K + sk) * BS;
-        Linv[idx] -= fl[sk];
-        Lqsr[idx] += fl[sk];
-        Lsht[idx] += fl[sk];
-        rem[sk] -= fl[sk];
-        done &= rem[sk] <= 0;
-        fsum += fl[sk];
-        fw += (double)fl[sk] * c.skw[sk];
-        if (dbg) {
-          if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] += fl[sk];
-          if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
+        for (int j = 0; j < WM; j++) {
+          const bool better = (cand >> j & 1u) && cst[j] < bc;
+          bc = better ? cst[j] : bc;
+          w = better ? j : w;
         }
+        cand &= ~(1u << w);
+        int fl[K];
+        bool any = false;
+#pragma unroll
+        for (int sk = 0; sk < K; sk++) {
+          const int iv = Linv[(w * K + sk) * BS];
+          fl[sk] = rem[sk] < iv ? rem[sk] : iv;
+          any |= fl[sk] > 0;
+        }
+        if (!any) continue;
+        double fw = 0.0;
+        int fsum = 0;
+        bool done = true;
+        unsigned need = 0u;
+#pragma unroll
+        for (int sk = 0; sk < K; sk++) {
+          const int idx = (w * K + sk) * BS;
+          const int left_inv = Linv[idx] - fl[sk];
+          Linv[idx] = left_inv;
+          Lqsr[idx] += fl[sk];
+          Lsht[idx] += fl[sk];
+          nz[sk] &= left_inv > 0 ? ~0u : ~(1u << w);
+          rem[sk] -= fl[sk];
+          done &= rem[sk] <= 0;
+          need |= rem[sk] > 0 ? nz[sk] : 0u;
+          fsum += fl[sk];
+          fw += (double)fl[sk] * c.skw[sk];
+          if (dbg) {
+            if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] += fl[sk];
+            if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
+          }
+        }
+        Lout[w * BS] += OF(r, w) + OV(r, w) * fw;
+        touched |= 1u << w;
+        used++;
+        if (dbg) {
+          if (info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] += 1;
+          if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] += fsum;
+        }
+        if (done) break;
+        cand &= need;  // only warehouses that still hold a needed SKU can contribute
       }
-      Lout[w * BS] += c.ofT[r * W + w] + c.ovT[r * W + w] * fw;
-      touched |= 1u << w;
-      used++;
-      if (dbg) {
-        if (info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] += 1;
-        if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] += fsum;
-      }
-      if (done) break;
     }
     bool anyrem = false;
 #pragma unroll
@@ -699,7 +1060,6 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
     }
     lost_cnt += anyrem ? 1 : 0;
   }
-  if (cur >= 0) finalize(cur);
 
   // ---- phase C: inventory, history, forecast, rewards, observations -------------------------
   const int hslot = t % MSC_HISTORY;
@@ -747,11 +1107,11 @@ __global__ __launch_bounds__(BS) void step_kernel(EnvConst c, EnvState s, StepIO
   const int64_t obs_off = e * W * c.L;
   if (!trunc) {
     s.t[e] = t + 1;
-    build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, io.obs + obs_off);
+    if (!(c.ablate & 1)) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, Lpipe, io.obs + obs_off);
   } else {
-    if (io.final_obs) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, io.final_obs + obs_off);
+    if (io.final_obs) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, Lpipe, io.final_obs + obs_off);
     reset_env<K>(c, s, e, 0, nullptr);
-    build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, io.obs + obs_off);
+    build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, Lpipe, io.obs + obs_off);
   }
 }
 
@@ -771,9 +1131,7 @@ __global__ void obs_flat_kernel(const float* __restrict__ obs, float* __restrict
 // ------------------------------------------------------------------------------------------
 int order_record_vec4(int K) { return (1 + K + 7) / 8; }
 
-size_t step_lds_bytes(const EnvConst& c) {
-  return (size_t)BS * (4 * (size_t)c.W * c.K * sizeof(int32_t) + 3 * (size_t)c.W * sizeof(double));
-}
+size_t step_lds_bytes(const EnvConst& c) { return step_lds_bytes_for(c, c.cost_lds != 0); }
 
 #define MSC_K_SWITCH(KV, BODY) \
   switch (KV) {                \
@@ -790,33 +1148,47 @@ size_t step_lds_bytes(const EnvConst& c) {
 
 static dim3 grid_for(int64_t E) { return dim3((unsigned)((E + BS - 1) / BS)); }
 
-hipError_t launch_reset(const EnvConst& c, const EnvState& s, const uint8_t* mask, const uint32_t* new_roots,
+hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask, const uint32_t* new_roots,
                         int32_t flags, float* obs, hipStream_t st) {
-  MSC_K_SWITCH(c.K, hipLaunchKernelGGL(reset_kernel<K>, grid_for(c.E), dim3(BS), 0, st, c, s, mask, new_roots, flags, obs));
-  return hipGetLastError();
-}
-
-hipError_t launch_demand(const EnvConst& c, const EnvState& s, hipStream_t st) {
-  MSC_K_SWITCH(c.K, hipLaunchKernelGGL(demand_poisson_kernel<K>, grid_for(c.E), dim3(BS), 0, st, c, s));
+  const size_t lds = (size_t)c.Lmax * c.K * BS * sizeof(int32_t);
+  MSC_K_SWITCH(c.K, hipLaunchKernelGGL(reset_kernel<K>, grid_for(c.E), dim3(BS), lds, st, d, mask, new_roots, flags, obs));
   return hipGetLastError();
 }
 
 template <int K>
-static hipError_t launch_step_k(const EnvConst& c, const EnvState& s, const StepIO& io, bool gen, hipStream_t st) {
-  const size_t lds = step_lds_bytes(c);
-  if (gen && c.demand_type == MSC_DEMAND_POISSON)
-    hipLaunchKernelGGL(demand_poisson_kernel<K>, grid_for(c.E), dim3(BS), 0, st, c, s);
-  if (c.W <= 4)
-    hipLaunchKernelGGL((step_kernel<K, 4>), grid_for(c.E), dim3(BS), lds, st, c, s, io);
-  else if (c.W <= 8)
-    hipLaunchKernelGGL((step_kernel<K, 8>), grid_for(c.E), dim3(BS), lds, st, c, s, io);
+static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st) {
+  const size_t lds = c.dem_lds ? (size_t)(2 + K) * c.R * sizeof(double) : 0;
+  if (c.demand_impl == 1)
+    hipLaunchKernelGGL(demand_poisson_nested_kernel<K>, grid_for(c.E), dim3(BS), 0, st, d);
+  else if (c.demand_impl == 2)
+    hipLaunchKernelGGL(demand_poisson_kernel<K>, grid_for(c.E), dim3(BS), lds, st, d);
+  else if (c.dem_lds)
+    hipLaunchKernelGGL((demand_flat_kernel<K, true>), grid_for(c.E), dim3(BS), lds, st, d);
   else
-    hipLaunchKernelGGL((step_kernel<K, 16>), grid_for(c.E), dim3(BS), lds, st, c, s, io);
+    hipLaunchKernelGGL((demand_flat_kernel<K, false>), grid_for(c.E), dim3(BS), 0, st, d);
+}
+
+hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st) {
+  MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st));
   return hipGetLastError();
 }
 
-hipError_t launch_step(const EnvConst& c, const EnvState& s, const StepIO& io, bool gen, hipStream_t st) {
-  MSC_K_SWITCH(c.K, return launch_step_k<K>(c, s, io, gen, st));
+template <int K>
+static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen, hipStream_t st) {
+  const size_t lds = step_lds_bytes(c);
+  if (gen && c.demand_type == MSC_DEMAND_POISSON) launch_demand_k<K>(c, d, st);
+  using KFn = void (*)(const DevEnv*, StepIO);
+  const bool t = c.cost_lds != 0;
+  KFn fn;
+  if (c.W <= 4) fn = t ? (KFn)step_kernel<K, 4, true> : (KFn)step_kernel<K, 4, false>;
+  else if (c.W <= 8) fn = t ? (KFn)step_kernel<K, 8, true> : (KFn)step_kernel<K, 8, false>;
+  else fn = t ? (KFn)step_kernel<K, 16, true> : (KFn)step_kernel<K, 16, false>;
+  hipLaunchKernelGGL(fn, grid_for(c.E), dim3(BS), lds, st, d, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_step(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen, hipStream_t st) {
+  MSC_K_SWITCH(c.K, return launch_step_k<K>(c, d, io, gen, st));
   return hipSuccess;
 }
 
