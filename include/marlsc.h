@@ -189,6 +189,12 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
  * No-op for the empirical sampler. */
 int msc_env_generate_demand(msc_env* env, msc_stream_t stream);
 
+/* Automatic demand pipelining (default on for the Poisson sampler): msc_env_step also launches the
+ * NEXT step's demand generation on a library-owned side stream, concurrent with the current step
+ * kernel (skipped across episode boundaries and after masked resets). Results are identical either
+ * way; 0 disables it (every step then runs demand + step back to back on the caller's stream). */
+int msc_env_set_pipelining(msc_env* env, int32_t enabled);
+
 /* Flat per-agent observation of the reference [E][W][L*(1+W)] = local_w || local_0..local_{W-1},
  * from the compact obs [E][W][L]. */
 int msc_env_obs_flat(const msc_env* env, const float* obs, float* flat, msc_stream_t stream);

@@ -43,9 +43,19 @@ struct msc_env {
   void* tables = nullptr;   // device copy of every static table
   void* arena = nullptr;    // persistent per-env state (checkpointed by save/load_state)
   size_t arena_bytes = 0;
-  void* scratch = nullptr;  // per-step order buffer
-  bool demand_ready = false;  // msc_env_generate_demand ran since the last step
-  DevEnv* dev = nullptr;      // device copy of {c, s}
+  void* scratch = nullptr;    // two per-step order buffers (double-buffered for pipelining)
+  size_t order_bytes = 0;     // bytes of one order buffer (records + counts)
+  DevEnv* dev = nullptr;      // device copies of {c, s}: dev[b] points at order buffer b
+  // Demand pipelining: the Poisson demand of step tau+1 depends only on each env's own demand
+  // stream, so it is generated on a side stream while the step kernel of tau runs (their waves
+  // co-reside on the CUs), unless step tau ends an episode (the in-kernel reset re-seeds the
+  // demand stream) or the envs' timesteps are out of sync after a masked reset.
+  hipStream_t side = nullptr;
+  hipEvent_t ev_dem[2] = {nullptr, nullptr}, ev_step[2] = {nullptr, nullptr}, ev_reset = nullptr;
+  int64_t tau = 0;                 // steps issued
+  int t_sync = -1;                 // common timestep of every env, -1 if unknown
+  bool ready[2] = {false, false};  // order buffer b holds the demand of the next step using it
+  bool pipeline = true;
 };
 
 extern "C" {
@@ -289,6 +299,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   const size_t a_fc = slot(sizeof(float) * WK * E);
   const size_t a_rng = slot(sizeof(uint64_t) * 8 * E);
   const size_t a_rbuf = slot(sizeof(uint32_t) * 4 * E);
+  const size_t a_rpre = slot(sizeof(uint64_t) * 4 * E);
+  const size_t a_bpre = slot(sizeof(uint32_t) * 2 * E);
   const size_t a_t = slot(sizeof(int32_t) * E);
   const size_t a_cnt = slot(sizeof(int32_t) * E);
   const size_t a_orig = slot(sizeof(uint32_t) * E);
@@ -308,17 +320,26 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   s.fc = (float*)(ab + a_fc);
   s.rng = (uint64_t*)(ab + a_rng);
   s.rbuf = (uint32_t*)(ab + a_rbuf);
+  s.rng_pre = (uint64_t*)(ab + a_rpre);
+  s.rbuf_pre = (uint32_t*)(ab + a_bpre);
   s.t = (int32_t*)(ab + a_t);
   s.counter = (int32_t*)(ab + a_cnt);
   s.orig_root = (uint32_t*)(ab + a_orig);
   s.root = (uint32_t*)(ab + a_root);
   s.emp_start = (int32_t*)(ab + a_emp);
   s.err = (uint32_t*)(ab + a_err);
+  EnvState s2 = s;
   if (d->demand_type == MSC_DEMAND_POISSON) {
-    const size_t sb = sizeof(uint4) * (size_t)nv * order_cap * E + sizeof(int32_t) * E + 256;
-    if (hipMalloc(&env->scratch, sb) != hipSuccess) return fail(set_err(-2, "hipMalloc(order buffer, %zu B) failed", sb));
-    s.orders = (uint4*)env->scratch;
-    s.n_orders = (int32_t*)((char*)env->scratch + sizeof(uint4) * (size_t)nv * order_cap * E);
+    const size_t rec_bytes = sizeof(uint4) * (size_t)nv * order_cap * E;
+    env->order_bytes = (rec_bytes + sizeof(int32_t) * E + 255) & ~size_t(255);
+    if (hipMalloc(&env->scratch, 2 * env->order_bytes) != hipSuccess)
+      return fail(set_err(-2, "hipMalloc(order buffers, %zu B) failed", 2 * env->order_bytes));
+    for (int b = 0; b < 2; b++) {
+      char* base = (char*)env->scratch + b * env->order_bytes;
+      EnvState& sb = b ? s2 : s;
+      sb.orders = (uint4*)base;
+      sb.n_orders = (int32_t*)(base + rec_bytes);
+    }
   }
   // root seeds: explicit, or SeedSequence([base_seed, worker_index, env_index])
   std::vector<uint32_t> roots(E);
@@ -341,11 +362,28 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   env->c = c;
   env->s = s;
   {
-    DevEnv hd{c, s};
-    if (hipMalloc(&env->dev, sizeof(DevEnv)) != hipSuccess ||
-        hipMemcpy(env->dev, &hd, sizeof(DevEnv), hipMemcpyHostToDevice) != hipSuccess)
+    DevEnv hd[2] = {{c, s}, {c, s2}};
+    if (hipMalloc(&env->dev, 2 * sizeof(DevEnv)) != hipSuccess ||
+        hipMemcpy(env->dev, hd, 2 * sizeof(DevEnv), hipMemcpyHostToDevice) != hipSuccess)
       return fail(set_err(-2, "device descriptor upload failed"));
   }
+  {
+    const char* pl = getenv("MSC_PIPELINE");
+    env->pipeline = !(pl && strcmp(pl, "0") == 0) && d->demand_type == MSC_DEMAND_POISSON;
+  }
+  if (hipStreamCreateWithFlags(&env->side, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_err(-2, "side stream creation failed"));
+  for (int b = 0; b < 2; b++)
+    if (hipEventCreateWithFlags(&env->ev_dem[b], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&env->ev_step[b], hipEventDisableTiming) != hipSuccess)
+      return fail(set_err(-2, "event creation failed"));
+  if (hipEventCreateWithFlags(&env->ev_reset, hipEventDisableTiming) != hipSuccess)
+    return fail(set_err(-2, "event creation failed"));
+  for (int b = 0; b < 2; b++) {  // recorded once so that every later wait is well-defined
+    (void)hipEventRecord(env->ev_dem[b], env->side);
+    (void)hipEventRecord(env->ev_step[b], env->side);
+  }
+  (void)hipEventRecord(env->ev_reset, env->side);
   *out = env;
   return 0;
 }
@@ -358,6 +396,12 @@ void msc_env_destroy(msc_env* env) {
   if (env->arena) (void)hipFree(env->arena);
   if (env->scratch) (void)hipFree(env->scratch);
   if (env->dev) (void)hipFree(env->dev);
+  for (int b = 0; b < 2; b++) {
+    if (env->ev_dem[b]) (void)hipEventDestroy(env->ev_dem[b]);
+    if (env->ev_step[b]) (void)hipEventDestroy(env->ev_step[b]);
+  }
+  if (env->ev_reset) (void)hipEventDestroy(env->ev_reset);
+  if (env->side) (void)hipStreamDestroy(env->side);
   delete env;
 }
 
@@ -377,8 +421,22 @@ int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t
 int msc_env_reset(msc_env* env, const uint8_t* mask, const uint32_t* new_root_seeds, int32_t flags, float* obs,
                   msc_stream_t stream) {
   if (!env) return set_err(-1, "null env");
-  env->demand_ready = false;  // a reset re-seeds the demand streams
-  HIP_TRY(launch_reset(env->c, env->dev, mask, new_root_seeds, flags, obs, (hipStream_t)stream));
+  hipStream_t st = (hipStream_t)stream;
+  // a reset re-seeds the demand streams: drop any demand generated ahead, order after the
+  // side stream's last use of the state
+  HIP_TRY(hipStreamWaitEvent(st, env->ev_dem[0], 0));
+  HIP_TRY(hipStreamWaitEvent(st, env->ev_dem[1], 0));
+  if (env->ready[0] || env->ready[1]) {
+    // envs outside the mask keep their episode: rewind their demand stream to before the
+    // dropped generation (rng[0][4][E] / rbuf[0][2][E] lead the arena's RNG slots)
+    const int64_t E = env->c.E;
+    HIP_TRY(hipMemcpyAsync(env->s.rng, env->s.rng_pre, sizeof(uint64_t) * 4 * E, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemcpyAsync(env->s.rbuf, env->s.rbuf_pre, sizeof(uint32_t) * 2 * E, hipMemcpyDeviceToDevice, st));
+  }
+  env->ready[0] = env->ready[1] = false;
+  env->t_sync = mask ? -1 : 0;
+  HIP_TRY(launch_reset(env->c, env->dev, mask, new_root_seeds, flags, obs, st));
+  HIP_TRY(hipEventRecord(env->ev_reset, st));
   return 0;
 }
 
@@ -411,16 +469,54 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
     for (auto& q : z)
       if (q.p) HIP_TRY(hipMemsetAsync(q.p, 0, q.n, st));
   }
-  HIP_TRY(launch_step(c, env->dev, io, !env->demand_ready, st));
-  env->demand_ready = false;
+  const bool poisson = c.demand_type == MSC_DEMAND_POISSON;
+  const int b = (int)(env->tau & 1);
+  if (poisson) {
+    if (env->ready[b]) {
+      HIP_TRY(hipStreamWaitEvent(st, env->ev_dem[b], 0));
+    } else {
+      HIP_TRY(launch_demand(c, env->dev + b, st));
+      HIP_TRY(hipEventRecord(env->ev_dem[b], st));
+    }
+  }
+  HIP_TRY(launch_step(c, env->dev + b, io, false, st));
+  HIP_TRY(hipEventRecord(env->ev_step[b], st));
+  env->ready[b] = false;
+  const bool boundary = env->t_sync < 0 || env->t_sync + 1 >= c.T;
+  if (env->pipeline && !boundary) {
+    // demand of step tau+1 into the other buffer, concurrently with this step kernel; that buffer
+    // was last read by step tau-1, and the demand stream was last advanced by demand(tau)
+    const int nb = b ^ 1;
+    HIP_TRY(hipStreamWaitEvent(env->side, env->ev_step[nb], 0));
+    HIP_TRY(hipStreamWaitEvent(env->side, env->ev_dem[b], 0));
+    HIP_TRY(hipStreamWaitEvent(env->side, env->ev_reset, 0));
+    HIP_TRY(launch_demand(c, env->dev + nb, env->side));
+    HIP_TRY(hipEventRecord(env->ev_dem[nb], env->side));
+    env->ready[nb] = true;
+  }
+  env->t_sync = env->t_sync < 0 ? -1 : (env->t_sync + 1 >= c.T ? 0 : env->t_sync + 1);
+  env->tau++;
+  return 0;
+}
+
+int msc_env_set_pipelining(msc_env* env, int32_t enabled) {
+  if (!env) return set_err(-1, "null env");
+  env->pipeline = enabled != 0 && env->c.demand_type == MSC_DEMAND_POISSON;
   return 0;
 }
 
 int msc_env_generate_demand(msc_env* env, msc_stream_t stream) {
   if (!env) return set_err(-1, "null env");
   if (env->c.demand_type != MSC_DEMAND_POISSON) return 0;
-  HIP_TRY(launch_demand(env->c, env->dev, (hipStream_t)stream));
-  env->demand_ready = true;
+  const int b = (int)(env->tau & 1);
+  if (env->ready[b]) return 0;  // already generated ahead
+  hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(hipStreamWaitEvent(st, env->ev_step[b], 0));     // last reader of buffer b
+  HIP_TRY(hipStreamWaitEvent(st, env->ev_dem[b ^ 1], 0));  // last advance of the demand streams
+  HIP_TRY(hipStreamWaitEvent(st, env->ev_reset, 0));
+  HIP_TRY(launch_demand(env->c, env->dev + b, st));
+  HIP_TRY(hipEventRecord(env->ev_dem[b], st));
+  env->ready[b] = true;
   return 0;
 }
 
@@ -447,6 +543,11 @@ int msc_env_read_state(const msc_env* env, int32_t* inv, int32_t* ts, int32_t* e
     std::vector<uint32_t> b(4 * E);
     HIP_TRY(hipMemcpy(r.data(), env->s.rng, sizeof(uint64_t) * 8 * E, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(b.data(), env->s.rbuf, sizeof(uint32_t) * 4 * E, hipMemcpyDeviceToHost));
+    if (env->ready[env->tau & 1]) {
+      // the next step's demand is already generated: report the demand stream as of before it
+      HIP_TRY(hipMemcpy(r.data(), env->s.rng_pre, sizeof(uint64_t) * 4 * E, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(b.data(), env->s.rbuf_pre, sizeof(uint32_t) * 2 * E, hipMemcpyDeviceToHost));
+    }
     for (int64_t e = 0; e < E; e++)
       for (int k = 0; k < 2; k++) {
         for (int j = 0; j < 4; j++) rng[(e * 2 + k) * 6 + j] = r[(k * 4 + j) * E + e];
@@ -457,19 +558,49 @@ int msc_env_read_state(const msc_env* env, int32_t* inv, int32_t* ts, int32_t* e
   return 0;
 }
 
-int64_t msc_env_state_bytes(const msc_env* env) { return env ? (int64_t)env->arena_bytes : -1; }
+// Checkpoint blob: {magic, pending, t_sync, reserved} | state arena | [order buffer of the next
+// step when its demand was already generated ahead (its RNG draws are then already consumed)].
+struct StateHeader {
+  uint32_t magic, pending;
+  int32_t t_sync, reserved;
+};
+constexpr uint32_t STATE_MAGIC = 0x4d534331u;  // "MSC1"
+
+int64_t msc_env_state_bytes(const msc_env* env) {
+  return env ? (int64_t)(sizeof(StateHeader) + env->arena_bytes + env->order_bytes) : -1;
+}
 
 int msc_env_save_state(const msc_env* env, void* buf) {
   if (!env || !buf) return set_err(-1, "null argument");
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(buf, env->arena, env->arena_bytes, hipMemcpyDeviceToHost));
+  const int b = (int)(env->tau & 1);
+  StateHeader h{STATE_MAGIC, env->ready[b] ? 1u : 0u, env->t_sync, 0};
+  memcpy(buf, &h, sizeof h);
+  char* p = (char*)buf + sizeof h;
+  HIP_TRY(hipMemcpy(p, env->arena, env->arena_bytes, hipMemcpyDeviceToHost));
+  if (h.pending)
+    HIP_TRY(hipMemcpy(p + env->arena_bytes, (char*)env->scratch + b * env->order_bytes, env->order_bytes,
+                      hipMemcpyDeviceToHost));
   return 0;
 }
 
 int msc_env_load_state(msc_env* env, const void* buf) {
   if (!env || !buf) return set_err(-1, "null argument");
+  StateHeader h;
+  memcpy(&h, buf, sizeof h);
+  if (h.magic != STATE_MAGIC) return set_err(-1, "not a libmarlsc state blob");
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(env->arena, buf, env->arena_bytes, hipMemcpyHostToDevice));
+  const char* p = (const char*)buf + sizeof h;
+  HIP_TRY(hipMemcpy(env->arena, p, env->arena_bytes, hipMemcpyHostToDevice));
+  const int b = (int)(env->tau & 1);
+  env->ready[0] = env->ready[1] = false;
+  if (h.pending) {
+    HIP_TRY(hipMemcpy((char*)env->scratch + b * env->order_bytes, p + env->arena_bytes, env->order_bytes,
+                      hipMemcpyHostToDevice));
+    env->ready[b] = true;
+    HIP_TRY(hipEventRecord(env->ev_dem[b], env->side));
+  }
+  env->t_sync = h.t_sync;
   return 0;
 }
 

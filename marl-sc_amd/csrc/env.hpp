@@ -66,6 +66,8 @@ struct EnvState {
   MSC_G float* fc;           // [WK][E]       EMA demand forecast (f32, multi_env.py:789-793)
   MSC_G uint64_t* rng;       // [2][4][E]     {demand, lead} x {s_hi, s_lo, i_hi, i_lo}
   MSC_G uint32_t* rbuf;      // [2][2][E]     {demand, lead} x {has32, u32}
+  MSC_G uint64_t* rng_pre;   // [4][E] demand-stream state before the last demand generation
+  MSC_G uint32_t* rbuf_pre;  // [2][E] (reported while the next step's demand is pre-generated)
   MSC_G int32_t* t;          // [E] timestep
   MSC_G int32_t* counter;    // [E] SeedManager._episode_counter
   MSC_G uint32_t* orig_root; // [E] SeedManager._original_root_seed

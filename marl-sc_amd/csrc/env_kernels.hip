@@ -90,6 +90,15 @@ __device__ __forceinline__ Pcg64 load_rng(const EnvState& s, int which, int64_t 
   r.u32 = s.rbuf[(int64_t)which * 2 * E + E + e];
   return r;
 }
+// the demand stream as it was before this demand generation (see EnvState::rng_pre)
+__device__ __forceinline__ void store_rng_pre(const EnvState& s, int64_t e, int64_t E, const Pcg64& r) {
+  s.rng_pre[e] = r.s_hi;
+  s.rng_pre[E + e] = r.s_lo;
+  s.rng_pre[2 * E + e] = r.i_hi;
+  s.rng_pre[3 * E + e] = r.i_lo;
+  s.rbuf_pre[e] = r.has32;
+  s.rbuf_pre[E + e] = r.u32;
+}
 __device__ __forceinline__ void store_rng(const EnvState& s, int which, int64_t e, int64_t E, const Pcg64& r) {
   uint64_t* b = s.rng + (int64_t)which * 4 * E + e;
   b[0] = r.s_hi;
@@ -381,6 +390,7 @@ __global__ __launch_bounds__(BS) void demand_flat_kernel(const DevEnv* __restric
   constexpr int NV = Rec<K>::NV;
   constexpr int NW = 2 * NV;
   Pcg64 rg = load_rng(s, 0, e, E);
+  store_rng_pre(s, e, E, rg);
   int st = PS_ORD, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0;
   unsigned mask = 0;
   double prod = 1.0, thr = To[0], p = Tp[0];
@@ -496,6 +506,7 @@ __global__ __launch_bounds__(BS) void demand_poisson_kernel(const DevEnv* __rest
   constexpr int NV = Rec<K>::NV;
   constexpr int NW = 2 * NV;  // 64-bit words of a record
   Pcg64 rg = load_rng(s, 0, e, E);
+  store_rng_pre(s, e, E, rg);
   int st = ST_REGION, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0;
   bool isq = false;
   unsigned mask = 0;
@@ -606,6 +617,7 @@ __global__ __launch_bounds__(BS) void demand_poisson_nested_kernel(const DevEnv*
   const int64_t E = c.E;
   constexpr int NV = Rec<K>::NV;
   Pcg64 rg = load_rng(s, 0, e, E);
+  store_rng_pre(s, e, E, rg);
   int n = 0;
   for (int r = 0; r < c.R; r++) {
     const double elo = c.enlam_o[r], p = c.p_sku[r];

@@ -119,6 +119,10 @@ class VecInventoryEnv:
         """Draw the next step's demand now (see msc_env_generate_demand); overlappable."""
         abi.check(abi.lib().msc_env_generate_demand(self._h, _stream()))
 
+    def set_pipelining(self, enabled: bool) -> None:
+        """Toggle the library's automatic next-step demand pipelining (results are identical)."""
+        abi.check(abi.lib().msc_env_set_pipelining(self._h, int(bool(enabled))))
+
     def alloc_info(self) -> Dict[str, torch.Tensor]:
         """Device buffers for msc_step_info (the reference's collect_step_info dict)."""
         E, W, K, R = self.n_envs, self.W, self.K, self.R
