@@ -31,7 +31,11 @@ struct EnvConst {
   int32_t cost_lds;     // 1: step kernel stages the [R][W] outbound cost tables in LDS
   int32_t dem_lds;      // 1: demand kernel stages the Poisson rate tables in LDS
   int32_t ablate;       // timing-only phase ablation bits (MSC_ABLATE env var); 0 in production
-  int32_t demand_impl;  // 0 = flat state machine (default), 1 = nested loops (MSC_DEMAND_IMPL=nested, A/B only)
+  int32_t demand_impl;  // 0 = generator/parser split (default); A/B only: 1 nested, 2 flat_branchy, 3 flat
+  int32_t demand_gen;   // generator waves per block of the split demand kernel (1 or 2)
+  int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
+  int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
+  int32_t epw_step;     // envs per 64-lane block of the step kernel
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;
@@ -46,6 +50,7 @@ struct EnvConst {
   const MSC_G double* inV;         // [W*K]
   const MSC_G double* enlam_o;     // [R]   exp(-lambda_orders) from the host libm
   const MSC_G double* p_sku;       // [R]
+  const MSC_G double* p_skip;      // [R]   U > p_skip[r] <=> U >= p_sku[r] (SKU not in the order), U in 2^-53 Z
   const MSC_G double* enlam_q;     // [R*K] exp(-lambda_quantity)
   const MSC_G int32_t* elt;        // [W*K] expected lead times
   const MSC_G int32_t* maxdev;     // [K] or [1]
@@ -118,6 +123,7 @@ hipError_t launch_step(const EnvConst& c, const DevEnv* d, const StepIO& io, boo
 hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st);
 hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hipStream_t st);
 size_t step_lds_bytes(const EnvConst& c);
+size_t demand_lds_bytes(const EnvConst& c);  // per block of the production demand kernel
 int order_record_vec4(int K);
 // gae.hip
 hipError_t launch_gae(const float* r, const float* v, const float* nv, const uint8_t* term, const uint8_t* trunc,

@@ -21,6 +21,23 @@
 
 namespace msc {
 
+#ifdef MSC_PROF
+// in-kernel cycle accounting (profiling builds only: make prof -> libmarlsc_prof.so)
+__device__ unsigned long long g_prof[16];
+#define PROF_DECL(v) unsigned long long v = 0
+#define PROF_NOW() ((unsigned long long)clock64())
+#define PROF_T(v) const unsigned long long v = PROF_NOW()
+#define PROF_ADD(v, x) (v) += (x)
+#define PROF_FLUSH(i, v) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[i], (v))
+#else
+#define PROF_DECL(v)
+#define PROF_NOW() 0ull
+#define PROF_T(v)
+#define PROF_ADD(v, x)
+#define PROF_FLUSH(i, v)
+#endif
+
 // Explicit global address space for hot buffers: pointers loaded from the device-resident DevEnv
 // are generic, and generic (flat_*) loads also count against lgkmcnt, so any LDS wait would also
 // wait for them and defeat software prefetching.
@@ -384,8 +401,8 @@ __global__ __launch_bounds__(BS) void demand_flat_kernel(const DevEnv* __restric
     Tp = lp;
     Tq = lq;
   }
-  const int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x;
-  if (e >= c.E) return;
+  const int64_t e = (int64_t)blockIdx.x * c.epw_dem + threadIdx.x;
+  if ((int)threadIdx.x >= c.epw_dem || e >= c.E) return;
   const int64_t E = c.E;
   constexpr int NV = Rec<K>::NV;
   constexpr int NW = 2 * NV;
@@ -462,6 +479,241 @@ __global__ __launch_bounds__(BS) void demand_flat_kernel(const DevEnv* __restric
     pre_p = Tp[rn];
   }
   store_rng(s, 0, e, E, rg);
+  if (n > cap) {
+    atomicOr(s.err, ERR_ORDER_OVERFLOW);
+    n = cap;
+  }
+  s.n_orders[e] = n;
+}
+
+// ------------------------------------------------------------------------------------------
+// Production demand kernel: generator waves + a parking parser.
+//
+// Measured on gfx950 (tools/ubench_rng.hip): one PCG64 draw costs ~88 ns per wave, but the flat
+// kernel above spends ~450 ns per draw, ~80 % of it in the sampler's state machine, which runs for
+// every lane on every draw because some lane of the 64 always changes state. Here a block owns
+// 64 envs with 1 + G waves:
+//   * generator waves 1..G advance each lane's PCG64 stream and write its uniforms into a
+//     per-lane LDS ring [DCAP][64] indexed by stream position (generator g of G writes positions
+//     g, g+G, ... using the G-step affine map of pcg_jump_coeffs);
+//   * the parser wave 0 splits the sampler into units that consume draws -- a Poisson loop
+//     (orders of a region, or one SKU quantity) or the K Bernoulli draws of an order's SKU mask --
+//     and the zero-draw bookkeeping between units. The hot loop only advances the current unit
+//     (prod *= U; compare; count) and PARKS a lane whose unit ended; once >= park_min lanes (or
+//     all live lanes) are parked, one settle pass handles all of them: record the quantity, emit
+//     the order, open the next SKU / order / region unit. The Bernoulli test U < p is folded into
+//     the same comparison (U > p_skip, prod = 1 in the mask unit).
+// Chunks of DCH hot iterations (each lane consumes <= 1 draw per iteration) are separated by one
+// barrier at which the parser publishes every lane's consumed count; the generators then refill
+// each lane's ring up to consumed + DCAP, which never touches a position the parser can still read
+// in the next chunk. The final stream state is the start state advanced by the consumed count.
+// ------------------------------------------------------------------------------------------
+#ifndef MSC_DCH
+#define MSC_DCH 16
+#endif
+constexpr int DCH = MSC_DCH;   // hot iterations per chunk
+constexpr int DCAP = 2 * DCH;  // per-lane ring capacity (draws)
+
+__host__ __device__ constexpr size_t park_lds_fixed() {
+  return (size_t)DCAP * BS * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
+}
+
+template <int K, int G, bool LDS_TAB>
+__global__ __launch_bounds__(BS * (1 + G)) void demand_park_kernel(const DevEnv* __restrict__ dp) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  const int R = c.R;
+  constexpr int NV = Rec<K>::NV;
+  constexpr int NW = 4 * NV;  // 32-bit words of an order record
+  extern __shared__ __attribute__((aligned(16))) double plds[];
+  __shared__ int more[2];
+  double* ring = plds;                                           // [DCAP][BS]
+  int32_t* rdv = reinterpret_cast<int32_t*>(plds + DCAP * BS);   // [2][BS] consumed draws per lane
+  const double* To = c.enlam_o;
+  const double* Tk = c.p_skip;
+  const double* Tq = c.enlam_q;
+  if constexpr (LDS_TAB) {
+    double* lo = plds + DCAP * BS + BS;  // after rdv (2*BS int32 = BS doubles)
+    double* lk = lo + R;
+    double* lq = lk + R;
+    for (int i = threadIdx.x; i < R; i += blockDim.x) {
+      lo[i] = c.enlam_o[i];
+      lk[i] = c.p_skip[i];
+    }
+    for (int i = threadIdx.x; i < R * K; i += blockDim.x) lq[i] = c.enlam_q[i];
+    To = lo;
+    Tk = lk;
+    Tq = lq;
+  }
+  const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;  // role is wave-uniform
+  const int64_t E = c.E;
+  const int64_t e = (int64_t)blockIdx.x * c.epw_dem + lane;
+  const bool valid = lane < c.epw_dem && e < E;
+
+  if (wave > 0) {
+    // ---------------- generator g: stream positions g, g + G, g + 2G, ...
+    const int g = wave - 1;
+    uint64_t th = 0, tl = 0, ih = 0, il = 1;
+    if (valid) {
+      Pcg64 rg = load_rng(s, 0, e, E);
+      for (int j = 0; j <= g; j++) pcg_step(rg);  // the state whose output is draw g
+      th = rg.s_hi;
+      tl = rg.s_lo;
+      ih = rg.i_hi;
+      il = rg.i_lo;
+    }
+    uint64_t mh = PCG_MUL_HI, ml = PCG_MUL_LO, ch = ih, cl = il;
+    if constexpr (G > 1) pcg_jump_coeffs(G, ih, il, mh, ml, ch, cl);
+    int pg = g;
+    auto gen_to = [&](int target) {
+      while (pg < target) {
+        ring[(pg & (DCAP - 1)) * BS + lane] = u64_to_double(pcg_output(th, tl));
+        uint64_t nh, nl;
+        mul128(th, tl, mh, ml, nh, nl);
+        add128(nh, nl, ch, cl);
+        th = nh;
+        tl = nl;
+        pg += G;
+      }
+    };
+    PROF_DECL(p_gen);
+    PROF_DECL(p_bar);
+    if (valid) gen_to(DCAP);
+    __syncthreads();
+    for (int ci = 0;; ci++) {
+      PROF_T(t0);
+      if (valid) gen_to(rdv[(ci & 1) * BS + lane] + DCAP);
+      PROF_T(t1);
+      __syncthreads();
+      PROF_ADD(p_gen, t1 - t0);
+      PROF_ADD(p_bar, PROF_NOW() - t1);
+      if (!more[ci & 1]) break;
+    }
+    PROF_FLUSH(8, p_gen);
+    PROF_FLUSH(9, p_bar);
+    return;
+  }
+
+  // ---------------- parser
+  Pcg64 r0{};
+  if (valid) {
+    r0 = load_rng(s, 0, e, E);
+    store_rng_pre(s, e, E, r0);
+  }
+  rdv[lane] = 0;
+  int st = valid ? PS_ORD : PS_DONE, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0, rd = 0;
+  unsigned mask = 0;
+  int pk = 0, mf = 0, live = valid ? 1 : 0;  // parked / unit is the SKU mask / not done (0 or 1)
+  uint32_t w[NW];
+#pragma unroll
+  for (int j = 0; j < NW; j++) w[j] = 0;
+  const int cap = c.order_cap;
+  const int pmin = c.park_min;
+  MSC_GLOBAL uint4* out = gp(s.orders + e);
+  __syncthreads();  // tables and the first DCAP draws of every lane are in LDS
+  double prod = 1.0, thr = To[0];
+  // settle pass over the parked lanes (branch-free apart from the record store): the lane's unit
+  // ended; book its result and open the next unit that consumes draws
+  auto settle = [&]() {
+    const bool is_ord = st == PS_ORD, is_qty = st == PS_QTY;
+    const uint32_t v = (uint32_t)(x > 1 ? x : 1);  // max(1, Poisson(lambda_q))
+    const int h = 1 + sq;
+#pragma unroll
+    for (int j = 0; j < NW; j++) w[j] |= (is_qty && (h >> 1) == j) ? v << (16 * (h & 1)) : 0u;
+    mask = is_qty ? (mask & (mask - 1u)) : mask;
+    const int nsq = mask ? __builtin_ctz(mask) : 0;
+    const int rn = r + 1 < R ? r + 1 : r;
+    const double q_thr = Tq[r * K + nsq], k_thr = Tk[r], o_thr = To[rn];  // speculative, one latency
+    const bool start_q = !is_ord && mask != 0;
+    const bool emit = !is_ord && mask == 0;  // order complete (possibly without SKUs)
+    if (emit && n < cap) {
+#pragma unroll
+      for (int j = 0; j < NV; j++)
+        gstore4(out, ((int64_t)n * NV + j) * E, make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]));
+    }
+    n += emit ? 1 : 0;
+    left = is_ord ? x : left - (emit ? 1 : 0);  // region r: Poisson(lambda_orders) orders
+    const bool start_order = !start_q && left > 0;
+    const bool next_region = !start_q && left <= 0;
+    const bool start_region = next_region && r + 1 < R;
+    r += start_region ? 1 : 0;
+    sq = start_q ? nsq : sq;
+    st = start_q ? PS_QTY : start_order ? PS_MASK : start_region ? PS_ORD : PS_DONE;
+    thr = start_q ? q_thr : start_order ? k_thr : o_thr;
+    mask = start_order ? 0u : mask;
+#pragma unroll
+    for (int j = 0; j < NW; j++) w[j] = start_order ? (j == 0 ? (uint32_t)r : 0u) : w[j];
+    prod = 1.0;
+    x = 0;
+    k = 0;
+    pk = 0;
+    mf = st == PS_MASK ? 1 : 0;
+    live = st != PS_DONE ? 1 : 0;
+  };
+  constexpr int Q = 4;  // draws read per lane per round (one LDS latency per round)
+  PROF_DECL(p_all);
+  PROF_DECL(p_set);
+  PROF_DECL(p_bar);
+  PROF_DECL(n_set);
+  PROF_DECL(n_round);
+  PROF_DECL(n_chunk);
+  PROF_T(t_start);
+  for (int ci = 0;; ci++) {
+    for (int rr = 0; rr < DCH / Q; rr++) {
+      double u[Q];
+#pragma unroll
+      for (int j = 0; j < Q; j++) u[j] = ring[((rd + j) & (DCAP - 1)) * BS + lane];
+      int cr = 0;  // draws this lane consumed in the round
+#pragma unroll
+      for (int j = 0; j < Q; j++) {
+        // ---- hot: advance the lane's current unit by one draw. Flags are 0/1 integers combined
+        // with VALU bit operations: SGPR lane-mask logic and exec branches (VCC -> SALU -> exec
+        // round trips) cost more than the arithmetic itself here.
+        double U = u[0];
+#pragma unroll
+        for (int m = 1; m <= j; m++) U = cr == m ? u[m] : U;
+        const int a = live & (pk ^ 1);  // lane consumes this draw
+        const double pu = prod * U;
+        const int ct = pu > thr ? 1 : 0;  // Poisson: product above exp(-lambda); mask: SKU not drawn
+        const int am = a & mf, ap = a & (mf ^ 1);
+        mask |= (unsigned)(am & (ct ^ 1)) << k;
+        k += am;
+        const int pc = ap & ct;
+        x += pc;
+        prod = pc ? pu : prod;
+        pk |= (am & ((k + (64 - K)) >> 6)) | (ap & (ct ^ 1));  // mask: k == K; Poisson: ended
+        cr += a;
+        const uint64_t pkm = __ballot(pk);
+        if (pkm != 0 && (__popcll(pkm) >= pmin || pkm == __ballot(live))) {
+          PROF_T(ts);
+          if (pk) settle();
+          PROF_ADD(p_set, PROF_NOW() - ts);
+          PROF_ADD(n_set, 1);
+        }
+      }
+      rd += cr;
+      PROF_ADD(n_round, 1);
+    }
+    const bool any = __ballot(st != PS_DONE) != 0;
+    rdv[((ci + 1) & 1) * BS + lane] = rd;
+    if (lane == 0) more[ci & 1] = any ? 1 : 0;
+    PROF_T(tb);
+    __syncthreads();
+    PROF_ADD(p_bar, PROF_NOW() - tb);
+    PROF_ADD(n_chunk, 1);
+    if (!any) break;
+  }
+  PROF_ADD(p_all, PROF_NOW() - t_start);
+  PROF_FLUSH(0, p_all);
+  PROF_FLUSH(1, p_set);
+  PROF_FLUSH(2, p_bar);
+  PROF_FLUSH(3, n_set);
+  PROF_FLUSH(4, n_round);
+  PROF_FLUSH(5, n_chunk);
+  PROF_FLUSH(6, 1ull);
+  if (!valid) return;
+  pcg_advance(r0, (uint64_t)rd);
+  store_rng(s, 0, e, E, r0);
   if (n > cap) {
     atomicOr(s.err, ERR_ORDER_OVERFLOW);
     n = cap;
@@ -673,7 +925,7 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
   const EnvState& s = dp->s;
   extern __shared__ __attribute__((aligned(16))) int32_t lds[];
   const int lane = threadIdx.x;
-  const int64_t e = (int64_t)blockIdx.x * BS + lane;
+  const int64_t e = (int64_t)blockIdx.x * c.epw_step + lane;
   const int64_t E = c.E;
   const int W = c.W, WK = W * K, R = c.R, RING = c.RING;
   // LDS: per-lane [field][idx][lane] arrays, then the block-shared outbound cost table
@@ -709,7 +961,7 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
     CLt = Tcl;
     HMt = Thm;
   }
-  if (e >= c.E) return;
+  if (lane >= c.epw_step || e >= c.E) return;
   auto OF = [&](int r, int w) -> double { return OFt[r * W + w]; };
   auto OV = [&](int r, int w) -> double { return OVt[r * W + w]; };
   const msc_step_info info = io.info;
@@ -1158,13 +1410,20 @@ size_t step_lds_bytes(const EnvConst& c) { return step_lds_bytes_for(c, c.cost_l
     default: return hipErrorInvalidValue; \
   }
 
-static dim3 grid_for(int64_t E) { return dim3((unsigned)((E + BS - 1) / BS)); }
+static dim3 grid_for(int64_t E, int epw = BS) { return dim3((unsigned)((E + epw - 1) / epw)); }
 
 hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask, const uint32_t* new_roots,
                         int32_t flags, float* obs, hipStream_t st) {
   const size_t lds = (size_t)c.Lmax * c.K * BS * sizeof(int32_t);
   MSC_K_SWITCH(c.K, hipLaunchKernelGGL(reset_kernel<K>, grid_for(c.E), dim3(BS), lds, st, d, mask, new_roots, flags, obs));
   return hipGetLastError();
+}
+
+static bool park_lds_tables(const EnvConst& c) {
+  return park_lds_fixed() + (size_t)(2 + c.K) * c.R * sizeof(double) <= 32 * 1024;
+}
+size_t demand_lds_bytes(const EnvConst& c) {
+  return park_lds_fixed() + (park_lds_tables(c) ? (size_t)(2 + c.K) * c.R * sizeof(double) : 0);
 }
 
 template <int K>
@@ -1174,10 +1433,21 @@ static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st) 
     hipLaunchKernelGGL(demand_poisson_nested_kernel<K>, grid_for(c.E), dim3(BS), 0, st, d);
   else if (c.demand_impl == 2)
     hipLaunchKernelGGL(demand_poisson_kernel<K>, grid_for(c.E), dim3(BS), lds, st, d);
-  else if (c.dem_lds)
-    hipLaunchKernelGGL((demand_flat_kernel<K, true>), grid_for(c.E), dim3(BS), lds, st, d);
-  else
-    hipLaunchKernelGGL((demand_flat_kernel<K, false>), grid_for(c.E), dim3(BS), 0, st, d);
+  else if (c.demand_impl == 3) {
+    if (c.dem_lds)
+      hipLaunchKernelGGL((demand_flat_kernel<K, true>), grid_for(c.E, c.epw_dem), dim3(BS), lds, st, d);
+    else
+      hipLaunchKernelGGL((demand_flat_kernel<K, false>), grid_for(c.E, c.epw_dem), dim3(BS), 0, st, d);
+  } else {
+    using DFn = void (*)(const DevEnv*);
+    const size_t fixed = park_lds_fixed();
+    const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
+    const bool t = park_lds_tables(c);
+    const int G = c.demand_gen == 1 ? 1 : 2;
+    DFn fn = G == 1 ? (t ? (DFn)demand_park_kernel<K, 1, true> : (DFn)demand_park_kernel<K, 1, false>)
+                    : (t ? (DFn)demand_park_kernel<K, 2, true> : (DFn)demand_park_kernel<K, 2, false>);
+    hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), fixed + (t ? tab : 0), st, d);
+  }
 }
 
 hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st) {
@@ -1195,7 +1465,7 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
   if (c.W <= 4) fn = t ? (KFn)step_kernel<K, 4, true> : (KFn)step_kernel<K, 4, false>;
   else if (c.W <= 8) fn = t ? (KFn)step_kernel<K, 8, true> : (KFn)step_kernel<K, 8, false>;
   else fn = t ? (KFn)step_kernel<K, 16, true> : (KFn)step_kernel<K, 16, false>;
-  hipLaunchKernelGGL(fn, grid_for(c.E), dim3(BS), lds, st, d, io);
+  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_step), dim3(BS), lds, st, d, io);
   return hipGetLastError();
 }
 
@@ -1210,5 +1480,16 @@ hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hip
   hipLaunchKernelGGL(obs_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, st, obs, flat, c.E, c.W, c.L);
   return hipGetLastError();
 }
+
+#ifdef MSC_PROF
+extern "C" int msc_debug_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 }  // namespace msc

@@ -114,6 +114,62 @@ MSC_HD uint32_t pcg_next32(Pcg64& r) {
 }
 MSC_HD double pcg_double(Pcg64& r) { return (double)(pcg_next64(r) >> 11) * (1.0 / 9007199254740992.0); }
 
+// ---- 128-bit LCG algebra for split / jump-ahead generation ----------------------------------
+// low 128 bits of (ah:al) * (bh:bl)
+MSC_HD void mul128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl, uint64_t& rh, uint64_t& rl) {
+  const uint64_t lo = al * bl;
+  rh = mulhi64(al, bl) + ah * bl + al * bh;
+  rl = lo;
+}
+MSC_HD void add128(uint64_t& ah, uint64_t& al, uint64_t bh, uint64_t bl) {
+  const uint64_t lo = al + bl;
+  ah += bh + (lo < bl ? 1u : 0u);
+  al = lo;
+}
+// XSL-RR output of a state and numpy's random() of it
+MSC_HD uint64_t pcg_output(uint64_t s_hi, uint64_t s_lo) {
+  const uint64_t x = s_hi ^ s_lo;
+  const unsigned rot = (unsigned)(s_hi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+MSC_HD double u64_to_double(uint64_t v) { return (double)(v >> 11) * (1.0 / 9007199254740992.0); }
+
+// Affine map s -> A*s + C of `n` PCG64 steps for increment (ih:il) (Brown, "Random number
+// generation with arbitrary strides"; numpy's pcg64_advance uses the same recurrence).
+MSC_HD void pcg_jump_coeffs(uint64_t n, uint64_t ih, uint64_t il, uint64_t& ah, uint64_t& al, uint64_t& ch,
+                            uint64_t& cl) {
+  uint64_t am_h = 0, am_l = 1, ap_h = 0, ap_l = 0;                 // accumulated map (identity)
+  uint64_t cm_h = PCG_MUL_HI, cm_l = PCG_MUL_LO, cp_h = ih, cp_l = il;  // map of 2^k steps
+  while (n) {
+    if (n & 1) {
+      uint64_t th, tl;
+      mul128(am_h, am_l, cm_h, cm_l, am_h, am_l);
+      mul128(ap_h, ap_l, cm_h, cm_l, th, tl);
+      add128(th, tl, cp_h, cp_l);
+      ap_h = th;
+      ap_l = tl;
+    }
+    uint64_t mh = cm_h, ml = cm_l;  // cp = (cm + 1) * cp ; cm = cm * cm
+    add128(mh, ml, 0, 1);
+    mul128(mh, ml, cp_h, cp_l, cp_h, cp_l);
+    mul128(cm_h, cm_l, cm_h, cm_l, cm_h, cm_l);
+    n >>= 1;
+  }
+  ah = am_h;
+  al = am_l;
+  ch = ap_h;
+  cl = ap_l;
+}
+// advance the stream by n draws of next64 (the 32-bit buffer is left as it is)
+MSC_HD void pcg_advance(Pcg64& r, uint64_t n) {
+  uint64_t ah, al, ch, cl, sh, sl;
+  pcg_jump_coeffs(n, r.i_hi, r.i_lo, ah, al, ch, cl);
+  mul128(ah, al, r.s_hi, r.s_lo, sh, sl);
+  add128(sh, sl, ch, cl);
+  r.s_hi = sh;
+  r.s_lo = sl;
+}
+
 // PCG64(SeedSequence pool): generate_state(4, uint64) = {seed_hi, seed_lo, inc_hi, inc_lo}
 MSC_HD void pcg_seed_pool(Pcg64& r, const uint32_t pool[4]) {
   uint32_t w[8];

@@ -72,7 +72,9 @@ class MscStepInfo(C.Structure):
 INFO_FIELDS_I32 = [f for f, t in MscStepInfo._fields_ if t is I32P]
 
 _LIB = None
-LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libmarlsc.so"
+# MSC_LIB_VARIANT=<name> selects an A/B or profiling build libmarlsc_<name>.so (make variant)
+_VARIANT = os.environ.get("MSC_LIB_VARIANT", "")
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / (f"libmarlsc_{_VARIANT}.so" if _VARIANT else "libmarlsc.so")
 
 
 def lib() -> C.CDLL:
