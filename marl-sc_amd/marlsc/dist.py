@@ -1,0 +1,50 @@
+"""Multi-GPU plumbing of the rollout: envs shard by global env id, one process per
+GPU, and the only collective on the path is the advantage-normalisation all-reduce.
+
+Env ids: rank g owns global env ids [g*E, (g+1)*E); every env's root seed derives from its global
+id (SeedManager.derive_env_seed(base, worker, global_id), base.py:377-431 of the reference), so an
+env's trajectory does not depend on the number of GPUs (weak scaling, no env-state exchange).
+
+Advantage normalisation: the GAE kernel accumulates [sum A, sum A^2, n] in f64 per rank; these
+24 bytes are SUM-all-reduced (RCCL over xGMI on MI355X, gloo on CPU) once per rollout, and every
+rank normalises with the global mean/std: (A - mean) / max(1e-4, std) (RLlib's standardisation).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> Tuple[int, int]:
+    """(rank, world_size) of the default process group, (0, 1) when not initialised."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def env_index_offset(envs_per_rank: int, rank: Optional[int] = None) -> int:
+    """First global env id of `rank` (weak scaling: every rank owns envs_per_rank envs)."""
+    r = world()[0] if rank is None else rank
+    return r * envs_per_rank
+
+
+def allreduce_adv_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place SUM all-reduce of the f64 [sum, sum_sq, n] advantage statistics."""
+    if stats.dtype != torch.float64 or stats.numel() != 3:
+        raise ValueError("advantage statistics must be a float64 tensor of 3 elements")
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM, group=group)
+    return stats
+
+
+def mean_std(stats: torch.Tensor) -> Tuple[float, float]:
+    """Global mean and (population) std from reduced [sum, sum_sq, n]."""
+    s, ss, n = (float(v) for v in stats.tolist())
+    if n <= 0:
+        raise ValueError("no advantages")
+    mean = s / n
+    var = max(ss / n - mean * mean, 0.0)
+    return mean, math.sqrt(var)

@@ -1,0 +1,205 @@
+"""CPU tests of the host side: the C ABI's exported surface, the 128-bit LCG algebra of rng.hpp,
+the folded Bernoulli threshold, config / seeding / trace host logic, and the world_size-2
+advantage-statistics all-reduce (gloo). No GPU calls."""
+import ctypes as C
+import os
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+HEADER = REPO / "include" / "marlsc.h"
+
+
+def header_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(msc_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_documented_entry_points():
+    fns = header_functions()
+    for must in ("msc_env_create", "msc_env_reset", "msc_env_step", "msc_env_obs_flat", "msc_gae",
+                 "msc_adv_normalize", "msc_last_error", "msc_env_destroy"):
+        assert must in fns
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    from marlsc import abi
+    L = abi.lib()  # dlopen only: no HIP call is made
+    missing = [f for f in header_functions() if not hasattr(L, f)]
+    assert not missing, missing
+    assert sorted(abi.EXPORTED_SYMBOLS) == header_functions()
+    m = re.search(r"#define\s+MSC_ABI_VERSION\s+(\d+)", HEADER.read_text())
+    assert L.msc_abi_version() == int(m.group(1))
+
+
+def test_seedseq_utility_matches_numpy():
+    from marlsc import abi
+    L = abi.lib()
+    for words in ([42], [123456789, 7], [987654321, 0, 5], [1, 2, 3, 4, 5]):
+        arr = (C.c_uint32 * len(words))(*words)
+        got = L.msc_seedseq_u32(arr, len(words))
+        want = int(np.random.SeedSequence(words).generate_state(1, dtype=np.uint32)[0])
+        assert got == want
+
+
+RNG_TEST = r"""
+#include <initializer_list>
+#include <cstdio>
+#include "rng.hpp"
+using namespace msc;
+int main() {
+  for (uint32_t root : {1u, 12345u, 4000000000u}) {
+    Pcg64 a; pcg_seed_child(a, root, 2);
+    for (uint64_t n : {0ull, 1ull, 2ull, 3ull, 63ull, 64ull, 1000ull, 8191ull}) {
+      Pcg64 b = a, c = a;
+      for (uint64_t i = 0; i < n; i++) pcg_step(b);
+      pcg_advance(c, n);
+      if (b.s_hi != c.s_hi || b.s_lo != c.s_lo) { printf("advance %llu\n", (unsigned long long)n); return 1; }
+    }
+    // G-step affine map used by the interleaved generator waves
+    for (int G : {1, 2, 3}) {
+      uint64_t mh, ml, ch, cl;
+      pcg_jump_coeffs(G, a.i_hi, a.i_lo, mh, ml, ch, cl);
+      Pcg64 b = a; uint64_t th = a.s_hi, tl = a.s_lo;
+      for (int k = 0; k < 20; k++) {
+        for (int j = 0; j < G; j++) pcg_step(b);
+        uint64_t nh, nl; mul128(th, tl, mh, ml, nh, nl); add128(nh, nl, ch, cl); th = nh; tl = nl;
+        if (th != b.s_hi || tl != b.s_lo) { printf("jump G=%d\n", G); return 1; }
+      }
+    }
+  }
+  puts("ok");
+  return 0;
+}
+"""
+
+
+def test_rng_jump_ahead_algebra(tmp_path):
+    src = tmp_path / "t.cpp"
+    src.write_text(RNG_TEST)
+    exe = tmp_path / "t"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-I", str(REPO / "marl-sc_amd" / "csrc"), str(src), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stdout
+
+
+def p_skip(p):
+    # capi.hip: ldexp(ceil(ldexp(p, 53)), -53) - 2^-53
+    return np.ldexp(np.ceil(np.ldexp(p, 53)), -53) - 2.0 ** -53
+
+
+@pytest.mark.parametrize("p", [0.667, 0.1, 0.5, 1.0, 1e-9, 0.3333333333333333, 0.9999999999999999, 2.0 ** -53])
+def test_folded_bernoulli_threshold(p):
+    # random() returns k * 2^-53; the kernels test `U > p_skip` for "SKU not drawn" (U >= p)
+    k0 = int(np.floor(p * 2.0 ** 53))
+    ks = np.arange(max(0, k0 - 3), min(2 ** 53, k0 + 4), dtype=np.int64)
+    U = ks.astype(np.float64) * 2.0 ** -53
+    assert np.array_equal(U < p, ~(U > p_skip(p)))
+
+
+def test_synthetic_config_and_spec():
+    from marlsc import EnvSpec, make_synthetic_env_config, validate_environment_config
+    cfg = make_synthetic_env_config(8, 64, 5)
+    validate_environment_config(cfg, allow_nr_ne_nw=True)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    assert (spec.W, spec.R, spec.K) == (8, 64, 5)
+    assert spec.local_obs_dim == 34  # L = (ns+1) + 3 ns + ns + nw at C3
+    assert spec.local_obs_dim * (1 + spec.W) == 306
+
+
+def test_config_validation_rejects_bad_values():
+    from marlsc import make_synthetic_env_config, validate_environment_config
+    cfg = make_synthetic_env_config(2, 4, 2)
+    bad = dict(cfg)
+    bad["n_warehouses"] = 0
+    with pytest.raises(Exception):
+        validate_environment_config(bad, allow_nr_ne_nw=True)
+
+
+def test_seed_manager_semantics():
+    from marlsc import SeedManager
+    sm = SeedManager(42)
+    t = sm.get_seed_int("train")
+    assert t == int(np.random.SeedSequence(42).spawn(6)[3].generate_state(1, dtype=np.uint32)[0])
+    e = SeedManager.derive_env_seed(t, 0, 5)
+    assert e == int(np.random.SeedSequence([t, 0, 5]).generate_state(1, dtype=np.uint32)[0])
+    env_sm = SeedManager(e, seed_registry=("preprocessing", "inventory", "demand_sampler", "lead_time_sampler"))
+    env_sm.advance_episode()
+    assert env_sm.root_seed == int(np.random.SeedSequence([e, 0]).generate_state(1, dtype=np.uint32)[0])
+    env_sm.advance_episode()
+    assert env_sm.root_seed == int(np.random.SeedSequence([e, 1]).generate_state(1, dtype=np.uint32)[0])
+
+
+def test_env_shards_have_disjoint_global_ids():
+    from marlsc.dist import env_index_offset
+    ids = [set(range(env_index_offset(1024, r), env_index_offset(1024, r) + 1024)) for r in range(8)]
+    assert sum(len(s) for s in ids) == len(set().union(*ids)) == 8192
+
+
+def _adv_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(REPO / "marl-sc_amd"))
+    from marlsc.dist import allreduce_adv_stats, mean_std
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full = torch.from_numpy(np.random.default_rng(0).normal(3.0, 2.0, 10_000))
+    part = full.chunk(world)[rank]
+    st = torch.tensor([part.sum().item(), (part * part).sum().item(), float(part.numel())], dtype=torch.float64)
+    allreduce_adv_stats(st)
+    m, s = mean_std(st)
+    normed = (part - m) / max(1e-4, s)
+    np.save(Path(out_dir) / f"r{rank}.npy", normed.numpy())
+    dist.destroy_process_group()
+
+
+def test_adv_norm_allreduce_world2_gloo(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_adv_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    got = np.concatenate([np.load(tmp_path / "r0.npy"), np.load(tmp_path / "r1.npy")])
+    full = np.random.default_rng(0).normal(3.0, 2.0, 10_000)
+    want = (full - full.mean()) / max(1e-4, full.std())
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+
+
+def test_trace_packer_matches_pandas_groupby():
+    # EmpiricalDemandSampler.sample (demand_sampler.py:214-261): rows of one timestep grouped by
+    # (region_id, order_id) -- pandas sorts the group keys -- quantities summed per SKU
+    import pandas as pd
+    from marlsc.trace import pack_demand_trace
+    rng = np.random.default_rng(3)
+    n = 3000
+    df = pd.DataFrame({
+        "timestep": rng.integers(0, 40, n),
+        "region_id": rng.integers(0, 16, n),
+        "order_id": [f"o{v}" for v in rng.integers(0, 400, n)],
+        "sku_id": rng.integers(0, 6, n),  # sku 5 is outside K=5 and must be dropped
+        "quantity": rng.integers(1, 9, n),
+    })
+    K = 5
+    tr = pack_demand_trace(df, K)
+    assert tr["n_rows"] == df["timestep"].nunique()
+    for i, t in enumerate(tr["timesteps"]):
+        sub = df[df["timestep"] == t]
+        want = []
+        for (reg, _), g in sub.groupby(["region_id", "order_id"]):
+            q = np.zeros(K, np.int64)
+            for s, v in zip(g["sku_id"], g["quantity"]):
+                if 0 <= s < K:
+                    q[s] += v
+            want.append((reg, q))
+        lo, hi = tr["offsets"][i], tr["offsets"][i + 1]
+        assert hi - lo == len(want)
+        for j, (reg, q) in enumerate(want):
+            assert tr["regions"][lo + j] == reg
+            assert np.array_equal(tr["quantities"][lo + j], q)
