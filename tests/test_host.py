@@ -203,3 +203,12 @@ def test_trace_packer_matches_pandas_groupby():
         for j, (reg, q) in enumerate(want):
             assert tr["regions"][lo + j] == reg
             assert np.array_equal(tr["quantities"][lo + j], q)
+
+
+@pytest.mark.parametrize("name,dims", [("env_c1_2wh4r2sku", (2, 4, 2, 13)), ("env_c3_8wh64r5sku", (8, 64, 5, 34)),
+                                       ("env_c5_16wh256r5sku", (16, 256, 5, 42))])
+def test_repo_config_files_load(name, dims):
+    from marlsc import EnvSpec, load_environment_config
+    cfg = load_environment_config(str(REPO / "config_files" / "environments" / f"{name}.yaml"), allow_nr_ne_nw=True)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True}, allow_nr_ne_nw=True)
+    assert (spec.W, spec.R, spec.K, spec.local_obs_dim) == dims
