@@ -1,16 +1,35 @@
-"""Summarise rocprofv3 PMC csv passes per kernel (mean over dispatches)."""
-import collections, csv, glob, sys
+"""Summarise rocprofv3 PMC csv passes per kernel (mean over dispatches) and write the per-launch
+HBM traffic of the env kernels to gpurun_out/traffic_<tag>.json.
+
+traffic = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): MI355X_MICROARCH.md "HBM [CDNA4]" -- on gfx950
+FETCH_SIZE reports half the bytes of wide coalesced reads (TCC_EA0_RDREQ x 64 B), WRITE_SIZE is
+exact for 16-B-per-lane stores."""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
 tag = sys.argv[1]
+workload = sys.argv[2] if len(sys.argv) > 2 else "8x64x5x32768"
 out = collections.defaultdict(dict)
-for path in glob.glob(f"gpurun_out/pmc_*_{tag}/pmc_counter_collection.csv"):
+for path in glob.glob(f"gpurun_out/pmc_*_{tag}/**/*counter_collection.csv", recursive=True):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for row in csv.DictReader(open(path)):
         acc[row["Kernel_Name"].split("(")[0]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     for k, v in acc.items():
         for c, x in v.items():
             out[k][c] = sum(x) / len(x)
-for k, v in out.items():
-    if "msc::" in k:
-        print(k)
-        for c in sorted(v):
-            print(f"   {c:24s} {v[c]:.6g}")
+traffic = {}
+for k, v in sorted(out.items()):
+    if "msc::" not in k:
+        continue
+    print(k)
+    for c in sorted(v):
+        print(f"   {c:24s} {v[c]:.6g}")
+    m = re.search(r"msc::(\w+)", k)
+    if m and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+        traffic[m.group(1)] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
+        print(f"   => HBM traffic per launch {traffic[m.group(1)] / 1e6:.2f} MB (2 x FETCH + WRITE)")
+json.dump({workload: traffic}, open(f"gpurun_out/traffic_{tag}.json", "w"), indent=1)
