@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "traffic.json"))
+    ap.add_argument("--rollout-T", type=int, default=100,
+                    help="steps of the MAPPO rollout line (0 = skip): env + actor/critic forward + buffers + GAE")
     args = ap.parse_args()
 
     import torch
@@ -163,10 +165,32 @@ def main():
     env.check()
     t_demand = sum(a.elapsed_time(b) for a, b, _ in evs) / KP / 1e3
     t_step = sum(b.elapsed_time(c) for _, b, c in evs) / KP / 1e3
-    tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    # (3) MAPPO rollout (configs[2]): env step + actor/critic forward + sampling + buffer writes +
+    #     GAE kernel + adv-norm statistics all-reduce, T steps per rollout
+    t_roll = 0.0
+    if args.rollout_T > 0:
+        import yaml
+        from marlsc.rollout import ActorCritic, RolloutCollector, RolloutConfig
+        rc = RolloutConfig.from_algorithm_config(yaml.safe_load(open(REPO / "config_files/algorithms/mappo.yaml")))
+        torch.manual_seed(0)
+        module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
+        col = RolloutCollector(env, module, args.rollout_T, seed=rank)
+        env.set_pipelining(True)
+        col.collect()  # warm-up (GEMM heuristics, allocator)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        col.collect()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t_roll = time.perf_counter() - t0
+        env.check()
+    tt = torch.tensor([dt, t_roll], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    dt = float(tt.item())
+    dt, t_roll = (float(x) for x in tt.tolist())
 
     if rank == 0:
         value = E * world * spec.W * K / dt
@@ -205,6 +229,14 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "bytes_per_launch": int(bytes_dom)},
         }
+        if args.rollout_T > 0:
+            out["rollout"] = {
+                "value": round(E * world * spec.W * args.rollout_T / t_roll, 1), "unit": "agent-steps/s",
+                "ms_per_step": round(t_roll / args.rollout_T * 1e3, 4), "T": args.rollout_T,
+                "policy": f"MAPPO (config_files/algorithms/mappo.yaml): actor {spec.local_obs_dim}-256-256-{spec.K}, "
+                          f"critic {spec.local_obs_dim * (1 + spec.W)}-64-64-1, fp32, parameter sharing",
+                "includes": "env step, obs_flat for the critic, actor+critic forward, Gaussian sampling, "
+                            "buffer writes, truncation bootstrap, GAE kernel, adv-norm all-reduce + normalise"}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
         print(json.dumps(out))

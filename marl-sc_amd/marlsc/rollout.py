@@ -1,0 +1,189 @@
+"""On-device rollout for IPPO / MAPPO: the actor/critic forward of the reference's RLModule in
+PyTorch-ROCm over the HIP env, and GAE + advantage normalisation in HIP.
+
+Reference structure restated (RLlib itself is not importable here, so this row is parity
+unpinned against the reference and checked against the numpy GAE in oracle/gae_ref.py):
+* `MLP`: `MLPArchitecture.build` (src/algorithms/models/architectures/mlp.py:14-60) -- Linear +
+  activation per hidden size, output Linear, optional output activation;
+* `ActorCritic`: `BaseRLModule._forward_inference/_forward_train/compute_values`
+  (src/algorithms/models/rlmodules/base.py:480-715) for MLP networks without shared layers --
+  actor on the local slice (or the full flat obs when actor_obs_type == "global"), free `log_std`
+  clamped at `logstd_floor` (`_append_log_std`), critic on local (IPPO) or full flat obs (MAPPO);
+* GAE(gamma, lambda) with truncation bootstrap V(final_obs) and RLlib's per-batch standardisation
+  `(A - mean) / max(1e-4, std)`, statistics all-reduced across ranks (marlsc/dist.py).
+
+Memory plan (288 GB HBM): the rollout stores the LOCAL observations only ([T, E, W, L] f32, 3.6 GB
+at C3); the MAPPO critic's flat input (local || global of the same env) is rebuilt on the device by
+`msc_env_obs_flat` when needed instead of storing [T, E, W, L(1+W)] (32 GB at C3).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Any, Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from . import abi
+from .dist import allreduce_adv_stats
+from .vec_env import VecInventoryEnv
+
+_ACT = {"relu": nn.ReLU, "tanh": nn.Tanh, "elu": nn.ELU, "gelu": nn.GELU, "sigmoid": nn.Sigmoid}
+
+
+def _act(name: str) -> nn.Module:
+    return _ACT.get(str(name).lower(), nn.ReLU)()
+
+
+class MLP(nn.Sequential):
+    def __init__(self, in_dim: int, out_dim: int, config: Dict[str, Any]):
+        layers, d = [], in_dim
+        for h in config.get("hidden_sizes", [128, 128]):
+            layers += [nn.Linear(d, h), _act(config.get("activation", "relu"))]
+            d = h
+        layers.append(nn.Linear(d, out_dim))
+        if config.get("output_activation"):
+            layers.append(_act(config["output_activation"]))
+        super().__init__(*layers)
+
+
+@dataclass
+class RolloutConfig:
+    gamma: float = 0.99
+    lam: float = 0.95
+    actor_obs_type: str = "local"
+    critic_obs_type: str = "global"
+    logstd_init: float = -1.0
+    logstd_floor: float = -3.5
+    actor: Optional[Dict[str, Any]] = None
+    critic: Optional[Dict[str, Any]] = None
+
+    @classmethod
+    def from_algorithm_config(cls, cfg: Dict[str, Any]) -> "RolloutConfig":
+        """From a config_files/algorithms/*.yaml dict (the reference's schema)."""
+        a = cfg.get("algorithm", cfg)
+        s = a.get("algorithm_specific", {})
+        nets = s.get("networks", {}) or {}
+        if nets.get("shared_layers"):
+            raise ValueError("shared_layers (GRU) networks are outside this build's rollout path")
+        for k in ("actor", "critic"):
+            if nets.get(k, {}).get("type", "mlp") != "mlp":
+                raise ValueError(f"{k}: only mlp networks are supported")
+        return cls(gamma=float(s.get("gamma", 0.99)), lam=float(s.get("lam", 0.95)),
+                   actor_obs_type=s.get("actor_obs_type", "local"),
+                   critic_obs_type=s.get("critic_obs_type", "global" if a.get("name") == "mappo" else "local"),
+                   logstd_init=float(s.get("logstd_init", -1.0)), logstd_floor=float(s.get("logstd_floor", -3.5)),
+                   actor=(nets.get("actor") or {}).get("config"), critic=(nets.get("critic") or {}).get("config"))
+
+
+class ActorCritic(nn.Module):
+    def __init__(self, local_obs_dim: int, global_obs_dim: int, action_dim: int, rc: RolloutConfig):
+        super().__init__()
+        self.local_obs_dim, self.rc = local_obs_dim, rc
+        full = local_obs_dim + global_obs_dim
+        self.actor = MLP(full if rc.actor_obs_type == "global" else local_obs_dim, action_dim,
+                         rc.actor or {"hidden_sizes": [256, 256]})
+        self.critic = MLP(full if rc.critic_obs_type == "global" else local_obs_dim, 1,
+                          rc.critic or {"hidden_sizes": [64, 64]})
+        self.log_std = nn.Parameter(torch.full((action_dim,), float(rc.logstd_init)))
+
+    def dist_inputs(self, local_obs: torch.Tensor, full_obs: Optional[torch.Tensor] = None):
+        """(mean, log_std) -- ACTION_DIST_INPUTS split in two."""
+        x = full_obs if self.rc.actor_obs_type == "global" else local_obs
+        mean = self.actor(x)
+        log_std = torch.clamp(self.log_std, min=self.rc.logstd_floor).expand_as(mean)
+        return mean, log_std
+
+    def values(self, local_obs: torch.Tensor, full_obs: Optional[torch.Tensor] = None) -> torch.Tensor:
+        x = full_obs if self.rc.critic_obs_type == "global" else local_obs
+        return self.critic(x).squeeze(-1)
+
+
+def _vp(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def gae(rewards, values, next_values, terminated, truncated, gamma, lam, adv=None, targets=None, stats=None):
+    """msc_gae over [T, N] (values [T+1, N]); returns (adv, targets, stats [sum, sum_sq, n] f64)."""
+    T, N = rewards.shape
+    for name, t, shape in (("rewards", rewards, (T, N)), ("values", values, (T + 1, N)),
+                           ("next_values", next_values, (T, N))):
+        if t.dtype != torch.float32 or not t.is_contiguous() or tuple(t.shape) != shape:
+            raise ValueError(f"{name}: expected contiguous float32 {shape}")
+    for name, t in (("terminated", terminated), ("truncated", truncated)):
+        if t.dtype != torch.uint8 or not t.is_contiguous() or tuple(t.shape) != (T, N):
+            raise ValueError(f"{name}: expected contiguous uint8 {(T, N)}")
+    adv = torch.empty_like(rewards) if adv is None else adv
+    targets = torch.empty_like(rewards) if targets is None else targets
+    stats = torch.zeros(3, dtype=torch.float64, device=rewards.device) if stats is None else stats.zero_()
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    abi.check(abi.lib().msc_gae(_vp(rewards), _vp(values), _vp(next_values), _vp(terminated), _vp(truncated), N, T,
+                                C.c_float(gamma), C.c_float(lam), _vp(adv), _vp(targets), _vp(stats), st))
+    return adv, targets, stats
+
+
+def normalize_advantages(adv: torch.Tensor, stats: torch.Tensor) -> torch.Tensor:
+    """In place (A - mean) / max(1e-4, std) with the (already all-reduced) statistics."""
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    abi.check(abi.lib().msc_adv_normalize(_vp(adv), adv.numel(), _vp(stats), st))
+    return adv
+
+
+class RolloutCollector:
+    """T steps of E envs x W agents (parameter sharing: one policy, N = E*W sequences)."""
+
+    def __init__(self, env: VecInventoryEnv, module: ActorCritic, T: int, *, seed: int = 0):
+        self.env, self.module, self.T = env, module, int(T)
+        E, W, K, L = env.n_envs, env.W, env.K, env.local_obs_dim
+        dev = env.device
+        self.N = E * W
+        self.obs = torch.empty((T, E, W, L), device=dev)
+        self.actions = torch.empty((T, E, W, K), device=dev)
+        self.logp = torch.empty((T, E, W), device=dev)
+        self.rewards = torch.empty((T, E, W), device=dev)
+        self.values = torch.empty((T + 1, E, W), device=dev)
+        self.next_values = torch.zeros((T, E, W), device=dev)
+        self.terminated = torch.zeros((T, E, W), dtype=torch.uint8, device=dev)
+        self.truncated = torch.zeros((T, E, W), dtype=torch.uint8, device=dev)
+        self.adv = torch.empty((T, E, W), device=dev)
+        self.targets = torch.empty((T, E, W), device=dev)
+        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        self._flat = torch.empty((E, W, L * (1 + W)), device=dev)
+        self._gen = torch.Generator(device=dev).manual_seed(seed)
+        self._need_flat = "global" in (module.rc.actor_obs_type, module.rc.critic_obs_type)
+
+    def _full(self, obs):
+        return self.env.obs_flat(obs=obs, out=self._flat) if self._need_flat else None
+
+    @torch.no_grad()
+    def collect(self, normalize: bool = True) -> Dict[str, torch.Tensor]:
+        env, m, T = self.env, self.module, self.T
+        obs = env.obs
+        for t in range(T):
+            self.obs[t].copy_(obs)
+            full = self._full(obs)
+            mean, log_std = m.dist_inputs(obs, full)
+            self.values[t] = m.values(obs, full)
+            std = log_std.exp()
+            a = mean + std * torch.randn(mean.shape, device=mean.device, generator=self._gen)
+            self.actions[t] = a
+            self.logp[t] = (-((a - mean) ** 2) / (2 * std * std) - log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+            obs, rew, trunc, final_obs = env.step(a.clamp_(-1.0, 1.0))
+            self.rewards[t] = rew
+            self.truncated[t] = trunc.unsqueeze(-1)
+            # truncation bootstrap: V(final_obs) for the envs whose episode ended at this step
+            full_f = self._full(final_obs)
+            self.next_values[t] = torch.where(trunc.bool().unsqueeze(-1), m.values(final_obs, full_f),
+                                              torch.zeros((), device=obs.device))
+        self.values[T] = m.values(obs, self._full(obs))
+        N = self.N
+        gae(self.rewards.view(T, N), self.values.view(T + 1, N), self.next_values.view(T, N),
+            self.terminated.view(T, N), self.truncated.view(T, N), m.rc.gamma, m.rc.lam,
+            self.adv.view(T, N), self.targets.view(T, N), self.stats)
+        if normalize:
+            allreduce_adv_stats(self.stats)
+            normalize_advantages(self.adv, self.stats)
+        return {"obs": self.obs, "actions": self.actions, "logp": self.logp, "rewards": self.rewards,
+                "values": self.values, "advantages": self.adv, "value_targets": self.targets}
