@@ -219,6 +219,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
                     : strcmp(impl, "nested") == 0       ? 1
                     : strcmp(impl, "flat_branchy") == 0 ? 2
                     : strcmp(impl, "flat") == 0         ? 3
+                    : strcmp(impl, "park1") == 0        ? 4
                                                         : 0;
     const char* gen = getenv("MSC_DEMAND_GEN");
     c.demand_gen = gen && atoi(gen) == 1 ? 1 : 2;

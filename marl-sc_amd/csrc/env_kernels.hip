@@ -721,6 +721,225 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_park_kernel(const DevEnv*
   s.n_orders[e] = n;
 }
 
+// ------------------------------------------------------------------------------------------
+// demand_park4_kernel: the parking parser with multi-draw hot steps (production default).
+//
+// Same generator / parser split and settle pass as demand_park_kernel, but one hot step advances
+// a lane's unit by up to PD = 4 draws at once: the Poisson products p1..p4 are chained
+// (prod*U0, p1*U1, ...), compared in parallel, and the lane consumes the leading run of
+// "continue" draws plus the ending draw; a mask unit takes min(4, K - k) Bernoulli draws (its
+// running product is reset to 1 before every multiply). The per-step overhead (the park check, the
+// LDS round trip for the lane's next uniforms) is thus paid once per ~3 draws instead of once per
+// draw. The ring is lane-major [64][DCAP4 + 1] (padded: conflict-free 8-B reads) so the four
+// consecutive positions a lane needs are independent reads issued right after the previous
+// step, overlapping the park check. A chunk is HS4 hot steps (<= PD * HS4 draws per lane).
+// ------------------------------------------------------------------------------------------
+constexpr int PD = 4;                // draws per hot step
+constexpr int HS4 = 4;               // hot steps per chunk
+constexpr int DCAP4 = 2 * PD * HS4;  // per-lane ring capacity (2 x the max draws of one chunk)
+constexpr int DSTR4 = DCAP4 + 1;     // padded lane stride (doubles)
+
+__host__ __device__ constexpr size_t park4_lds_fixed() {
+  return (size_t)BS * DSTR4 * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
+}
+
+template <int K, int G, bool LDS_TAB>
+__global__ __launch_bounds__(BS * (1 + G)) void demand_park4_kernel(const DevEnv* __restrict__ dp) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  const int R = c.R;
+  constexpr int NV = Rec<K>::NV;
+  constexpr int NW = 4 * NV;
+  extern __shared__ __attribute__((aligned(16))) double plds[];
+  __shared__ int more[2];
+  double* ring = plds;                                              // [BS][DSTR4]
+  int32_t* rdv = reinterpret_cast<int32_t*>(plds + BS * DSTR4);     // [2][BS]
+  const double* To = c.enlam_o;
+  const double* Tk = c.p_skip;
+  const double* Tq = c.enlam_q;
+  if constexpr (LDS_TAB) {
+    double* lo = plds + BS * DSTR4 + BS;
+    double* lk = lo + R;
+    double* lq = lk + R;
+    for (int i = threadIdx.x; i < R; i += blockDim.x) {
+      lo[i] = c.enlam_o[i];
+      lk[i] = c.p_skip[i];
+    }
+    for (int i = threadIdx.x; i < R * K; i += blockDim.x) lq[i] = c.enlam_q[i];
+    To = lo;
+    Tk = lk;
+    Tq = lq;
+  }
+  const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;
+  const int64_t E = c.E;
+  const int64_t e = (int64_t)blockIdx.x * c.epw_dem + lane;
+  const bool valid = lane < c.epw_dem && e < E;
+  double* myring = ring + lane * DSTR4;
+
+  if (wave > 0) {
+    // ---------------- generator g: stream positions g, g + G, g + 2G, ...
+    const int g = wave - 1;
+    uint64_t th = 0, tl = 0, ih = 0, il = 1;
+    if (valid) {
+      Pcg64 rg = load_rng(s, 0, e, E);
+      for (int j = 0; j <= g; j++) pcg_step(rg);
+      th = rg.s_hi;
+      tl = rg.s_lo;
+      ih = rg.i_hi;
+      il = rg.i_lo;
+    }
+    uint64_t mh = PCG_MUL_HI, ml = PCG_MUL_LO, ch = ih, cl = il;
+    if constexpr (G > 1) pcg_jump_coeffs(G, ih, il, mh, ml, ch, cl);
+    int pg = g;
+    auto gen_to = [&](int target) {
+      while (pg < target) {
+        myring[pg & (DCAP4 - 1)] = u64_to_double(pcg_output(th, tl));
+        uint64_t nh, nl;
+        mul128(th, tl, mh, ml, nh, nl);
+        add128(nh, nl, ch, cl);
+        th = nh;
+        tl = nl;
+        pg += G;
+      }
+    };
+    if (valid) gen_to(DCAP4);
+    __syncthreads();
+    for (int ci = 0;; ci++) {
+      if (valid) gen_to(rdv[(ci & 1) * BS + lane] + DCAP4);
+      __syncthreads();
+      if (!more[ci & 1]) break;
+    }
+    return;
+  }
+
+  // ---------------- parser
+  Pcg64 r0{};
+  if (valid) {
+    r0 = load_rng(s, 0, e, E);
+    store_rng_pre(s, e, E, r0);
+  }
+  rdv[lane] = 0;
+  int st = valid ? PS_ORD : PS_DONE, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0, rd = 0;
+  unsigned mask = 0;
+  int pk = 0, mf = 0, live = valid ? 1 : 0;
+  uint32_t w[NW];
+#pragma unroll
+  for (int j = 0; j < NW; j++) w[j] = 0;
+  const int cap = c.order_cap;
+  const int pmin = c.park_min;
+  MSC_GLOBAL uint4* out = gp(s.orders + e);
+  __syncthreads();
+  double prod = 1.0, thr = To[0];
+  auto settle = [&]() {
+    const bool is_ord = st == PS_ORD, is_qty = st == PS_QTY;
+    const uint32_t v = (uint32_t)(x > 1 ? x : 1);  // max(1, Poisson(lambda_q))
+    const int h = 1 + sq;
+#pragma unroll
+    for (int j = 0; j < NW; j++) w[j] |= (is_qty && (h >> 1) == j) ? v << (16 * (h & 1)) : 0u;
+    mask = is_qty ? (mask & (mask - 1u)) : mask;
+    const int nsq = mask ? __builtin_ctz(mask) : 0;
+    const int rn = r + 1 < R ? r + 1 : r;
+    const double q_thr = Tq[r * K + nsq], k_thr = Tk[r], o_thr = To[rn];
+    const bool start_q = !is_ord && mask != 0;
+    const bool emit = !is_ord && mask == 0;
+    if (emit && n < cap) {
+#pragma unroll
+      for (int j = 0; j < NV; j++)
+        gstore4(out, ((int64_t)n * NV + j) * E, make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]));
+    }
+    n += emit ? 1 : 0;
+    left = is_ord ? x : left - (emit ? 1 : 0);
+    const bool start_order = !start_q && left > 0;
+    const bool next_region = !start_q && left <= 0;
+    const bool start_region = next_region && r + 1 < R;
+    r += start_region ? 1 : 0;
+    sq = start_q ? nsq : sq;
+    st = start_q ? PS_QTY : start_order ? PS_MASK : start_region ? PS_ORD : PS_DONE;
+    thr = start_q ? q_thr : start_order ? k_thr : o_thr;
+    mask = start_order ? 0u : mask;
+#pragma unroll
+    for (int j = 0; j < NW; j++) w[j] = start_order ? (j == 0 ? (uint32_t)r : 0u) : w[j];
+    prod = 1.0;
+    x = 0;
+    k = 0;
+    pk = 0;
+    mf = st == PS_MASK ? 1 : 0;
+    live = st != PS_DONE ? 1 : 0;
+  };
+  PROF_DECL(p_all);
+  PROF_DECL(p_set);
+  PROF_DECL(p_bar);
+  PROF_DECL(n_set);
+  PROF_DECL(n_round);
+  PROF_DECL(n_chunk);
+  PROF_T(t_start);
+  for (int ci = 0;; ci++) {
+    double u0 = myring[rd & (DCAP4 - 1)], u1 = myring[(rd + 1) & (DCAP4 - 1)];
+    double u2 = myring[(rd + 2) & (DCAP4 - 1)], u3 = myring[(rd + 3) & (DCAP4 - 1)];
+#pragma unroll
+    for (int hs = 0; hs < HS4; hs++) {
+      // ---- hot step: up to PD draws of the lane's current unit
+      const int a = live & (pk ^ 1);
+      const double one = 1.0;
+      const double p1 = prod * u0;
+      const double p2 = (mf ? one : p1) * u1;
+      const double p3 = (mf ? one : p2) * u2;
+      const double p4 = (mf ? one : p3) * u3;
+      const int c1 = p1 > thr ? 1 : 0, c2 = p2 > thr ? 1 : 0, c3 = p3 > thr ? 1 : 0, c4 = p4 > thr ? 1 : 0;
+      // Poisson unit: leading run of continues, then the ending draw
+      const int n2 = c1 & c2, n3 = n2 & c3, n4 = n3 & c4;
+      const int ncont = c1 + n2 + n3 + n4;
+      // mask unit: take min(PD, K - k) Bernoulli draws; bit set = SKU drawn (U < p <=> !(U > p_skip))
+      const int take = (K - k) < PD ? (K - k) : PD;
+      const unsigned bits = (unsigned)((c1 ^ 1) | ((c2 ^ 1) << 1) | ((c3 ^ 1) << 2) | ((c4 ^ 1) << 3)) & ((1u << take) - 1u);
+      const int am = a & mf, ap = a & (mf ^ 1);
+      mask |= am ? bits << k : 0u;
+      k += am ? take : 0;
+      x += ap ? ncont : 0;
+      prod = (ap & n4) ? p4 : prod;
+      const int cons = mf ? take : (n4 ? PD : ncont + 1);
+      pk |= (am & ((k + (64 - K)) >> 6)) | (ap & (n4 ^ 1));
+      rd += a ? cons : 0;
+      u0 = myring[rd & (DCAP4 - 1)];
+      u1 = myring[(rd + 1) & (DCAP4 - 1)];
+      u2 = myring[(rd + 2) & (DCAP4 - 1)];
+      u3 = myring[(rd + 3) & (DCAP4 - 1)];
+      const uint64_t pkm = __ballot(pk);
+      if (pkm != 0 && (__popcll(pkm) >= pmin || pkm == __ballot(live))) {
+        PROF_T(ts);
+        if (pk) settle();
+        PROF_ADD(p_set, PROF_NOW() - ts);
+        PROF_ADD(n_set, 1);
+      }
+      PROF_ADD(n_round, 1);
+    }
+    const bool any = __ballot(st != PS_DONE) != 0;
+    rdv[((ci + 1) & 1) * BS + lane] = rd;
+    if (lane == 0) more[ci & 1] = any ? 1 : 0;
+    PROF_T(tb);
+    __syncthreads();
+    PROF_ADD(p_bar, PROF_NOW() - tb);
+    PROF_ADD(n_chunk, 1);
+    if (!any) break;
+  }
+  PROF_ADD(p_all, PROF_NOW() - t_start);
+  PROF_FLUSH(0, p_all);
+  PROF_FLUSH(1, p_set);
+  PROF_FLUSH(2, p_bar);
+  PROF_FLUSH(3, n_set);
+  PROF_FLUSH(4, n_round);
+  PROF_FLUSH(5, n_chunk);
+  PROF_FLUSH(6, 1ull);
+  if (!valid) return;
+  pcg_advance(r0, (uint64_t)rd);
+  store_rng(s, 0, e, E, r0);
+  if (n > cap) {
+    atomicOr(s.err, ERR_ORDER_OVERFLOW);
+    n = cap;
+  }
+  s.n_orders[e] = n;
+}
+
 // Variant with branchy settling (kept for A/B measurement: MSC_DEMAND_IMPL=flat_branchy).
 //
 // The reference's draw sequence per step is: for each region, Poisson(lambda_o) (multiplication
@@ -1419,11 +1638,12 @@ hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask,
   return hipGetLastError();
 }
 
+static size_t park_fixed(const EnvConst& c) { return c.demand_impl == 4 ? park_lds_fixed() : park4_lds_fixed(); }
 static bool park_lds_tables(const EnvConst& c) {
-  return park_lds_fixed() + (size_t)(2 + c.K) * c.R * sizeof(double) <= 32 * 1024;
+  return park_fixed(c) + (size_t)(2 + c.K) * c.R * sizeof(double) <= 32 * 1024;
 }
 size_t demand_lds_bytes(const EnvConst& c) {
-  return park_lds_fixed() + (park_lds_tables(c) ? (size_t)(2 + c.K) * c.R * sizeof(double) : 0);
+  return park_fixed(c) + (park_lds_tables(c) ? (size_t)(2 + c.K) * c.R * sizeof(double) : 0);
 }
 
 template <int K>
@@ -1440,12 +1660,17 @@ static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st) 
       hipLaunchKernelGGL((demand_flat_kernel<K, false>), grid_for(c.E, c.epw_dem), dim3(BS), 0, st, d);
   } else {
     using DFn = void (*)(const DevEnv*);
-    const size_t fixed = park_lds_fixed();
+    const size_t fixed = park_fixed(c);
     const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
     const bool t = park_lds_tables(c);
     const int G = c.demand_gen == 1 ? 1 : 2;
-    DFn fn = G == 1 ? (t ? (DFn)demand_park_kernel<K, 1, true> : (DFn)demand_park_kernel<K, 1, false>)
-                    : (t ? (DFn)demand_park_kernel<K, 2, true> : (DFn)demand_park_kernel<K, 2, false>);
+    DFn fn;
+    if (c.demand_impl == 4)  // single-draw hot steps (A/B: MSC_DEMAND_IMPL=park1)
+      fn = G == 1 ? (t ? (DFn)demand_park_kernel<K, 1, true> : (DFn)demand_park_kernel<K, 1, false>)
+                  : (t ? (DFn)demand_park_kernel<K, 2, true> : (DFn)demand_park_kernel<K, 2, false>);
+    else
+      fn = G == 1 ? (t ? (DFn)demand_park4_kernel<K, 1, true> : (DFn)demand_park4_kernel<K, 1, false>)
+                  : (t ? (DFn)demand_park4_kernel<K, 2, true> : (DFn)demand_park4_kernel<K, 2, false>);
     hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), fixed + (t ? tab : 0), st, d);
   }
 }
