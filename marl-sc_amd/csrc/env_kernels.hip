@@ -1181,8 +1181,18 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
     HMt = Thm;
   }
   if (lane >= c.epw_step || e >= c.E) return;
-  auto OF = [&](int r, int w) -> double { return OFt[r * W + w]; };
-  auto OV = [&](int r, int w) -> double { return OVt[r * W + w]; };
+  // outbound cost rows of the region being allocated, cached in registers at each region change
+  // (orders are region-major): the allocator's per-order costs need no table reads
+  double cof[WM], cov[WM];
+#pragma unroll
+  for (int w = 0; w < WM; w++) cof[w] = cov[w] = 0.0;
+  auto load_costs = [&](int r) {
+#pragma unroll
+    for (int w = 0; w < WM; w++) {
+      cof[w] = w < W ? OFt[r * W + w] : 0.0;
+      cov[w] = w < W ? OVt[r * W + w] : 0.0;
+    }
+  };
   const msc_step_info info = io.info;
   const bool dbg = io.has_info != 0;
 
@@ -1362,7 +1372,7 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
         double lg[WM], mx = -INFINITY, se = 0.0;
 #pragma unroll
         for (int w = 0; w < WM; w++) {
-          lg[w] = w < W ? -(OF(r, w) * (double)lost_cnt + OV(r, w) * lw) / c.alpha : -INFINITY;
+          lg[w] = w < W ? -(cof[w] * (double)lost_cnt + cov[w] * lw) / c.alpha : -INFINITY;  // r == cached region
           mx = lg[w] > mx ? lg[w] : mx;
         }
 #pragma unroll
@@ -1425,13 +1435,23 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
   // the loads stay in flight); the loop runs once past the last order as a sentinel so the region
   // epilogue has a single call site
   constexpr int NVR = Rec<K>::NV;
-  constexpr int PF = 4;
+#ifndef MSC_PF
+#define MSC_PF 4
+#endif
+  constexpr int PF = MSC_PF;
   uint4 ring[PF][NVR];
 #pragma unroll
   for (int q = 0; q < PF; q++)
 #pragma unroll
     for (int j = 0; j < NVR; j++) ring[q][j] = (q < n_orders) ? gload4(src, q * rec_step + j * stride) : make_uint4(0, 0, 0, 0);
+  PROF_DECL(sp_loop);
+  PROF_DECL(sp_fin);
+  PROF_DECL(sp_alloc);
+  PROF_DECL(sn_iter);
+  PROF_DECL(sn_fin);
+  PROF_T(ts_loop);
   for (int oi = 0; oi <= n_orders; oi++) {
+    PROF_ADD(sn_iter, 1);
     int r = -1;
     int d[K];
     {
@@ -1454,7 +1474,11 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
       for (int j = 0; j < NVR; j++) ring[PF - 1][j] = gload4(src, (oi + PF) * rec_step + j * stride);
     }
     if (r != cur) {
+      PROF_T(ts_fin);
       if (cur >= 0) finalize(cur);
+      PROF_ADD(sp_fin, PROF_NOW() - ts_fin);
+      PROF_ADD(sn_fin, 1);
+      if (r >= 0) load_costs(r);
       cur = r;
       lost_cnt = 0;
       touched = 0;
@@ -1478,10 +1502,11 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
       rem[sk] = d[sk];
       cand |= d[sk] > 0 ? nz[sk] : 0u;
     }
+    PROF_T(ts_alloc);
     if (cand) {
       double cst[WM];  // cost = fixed + variable * order weight (demand_allocator.py:168-172)
 #pragma unroll
-      for (int w = 0; w < WM; w++) cst[w] = (w < W && (cand >> w & 1u)) ? OF(r, w) + OV(r, w) * tw : INFINITY;
+      for (int w = 0; w < WM; w++) cst[w] = (w < W && (cand >> w & 1u)) ? cof[w] + cov[w] * tw : INFINITY;
       int used = 0;
       while (cand && used < maxwh) {
         int w = 0;
@@ -1524,7 +1549,17 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
             if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
           }
         }
-        Lout[w * BS] += OF(r, w) + OV(r, w) * fw;
+        if (fw == tw) {
+          Lout[w * BS] += bc;  // whole order from w: the ranking cost is of + ov * tw bit for bit
+        } else {
+          double ofw = 0.0, ovw = 0.0;
+#pragma unroll
+          for (int j = 0; j < WM; j++) {
+            ofw = j == w ? cof[j] : ofw;
+            ovw = j == w ? cov[j] : ovw;
+          }
+          Lout[w * BS] += ofw + ovw * fw;
+        }
         touched |= 1u << w;
         used++;
         if (dbg) {
@@ -1535,6 +1570,7 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
         cand &= need;  // only warehouses that still hold a needed SKU can contribute
       }
     }
+    PROF_ADD(sp_alloc, PROF_NOW() - ts_alloc);
     bool anyrem = false;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
@@ -1543,6 +1579,13 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
     }
     lost_cnt += anyrem ? 1 : 0;
   }
+  PROF_ADD(sp_loop, PROF_NOW() - ts_loop);
+  PROF_FLUSH(10, sp_loop);
+  PROF_FLUSH(11, sp_fin);
+  PROF_FLUSH(12, sp_alloc);
+  PROF_FLUSH(13, sn_iter);
+  PROF_FLUSH(14, sn_fin);
+  PROF_FLUSH(15, 1ull);
 
   // ---- phase C: inventory, history, forecast, rewards, observations -------------------------
   const int hslot = t % MSC_HISTORY;

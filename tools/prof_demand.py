@@ -51,3 +51,6 @@ print(f"settles/wave {per(3):.0f}  rounds/wave {per(4):.0f}  chunks/wave {per(5)
 print(f"cycles per settle {v[1]/max(v[3],1):.0f}; per round (excl settles) {(v[0]-v[1]-v[2])/max(v[4],1):.0f}")
 gw = max(waves, 1) * int(os.environ.get("GEN", "2"))
 print(f"generator cycles/wave: gen {v[8]/N/gw:.0f}  barrier {v[9]/N/gw:.0f}")
+sw = max(v[15] / N, 1)
+print(f"step kernel cycles/wave: order loop {v[10]/N/sw:.0f}  finalize {v[11]/N/sw:.0f}  allocation {v[12]/N/sw:.0f}  "
+      f"iterations {v[13]/N/sw:.0f}  finalize passes {v[14]/N/sw:.0f}")
