@@ -97,9 +97,9 @@ struct StepIO {
 constexpr uint32_t ERR_ORDER_OVERFLOW = 1u;
 
 // int32 words of the step kernel's per-lane LDS arrays (inventory, shipped-to-region,
-// shipped-total, shipped-home: 4*W*K; pipeline buckets: Lmax*K), rounded to 16 B.
+// shipped-total, shipped-home: 4*W*K), rounded to 16 B.
 __host__ __device__ inline int step_lds_ints(const EnvConst& c) {
-  const int n = (4 * c.W * c.K + c.Lmax * c.K) * BS;
+  const int n = (4 * c.W * c.K) * BS;
   return (n + 3) & ~3;
 }
 // total dynamic LDS of the step kernel, with or without the shared outbound cost table

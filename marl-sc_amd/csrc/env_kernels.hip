@@ -189,17 +189,18 @@ __device__ __noinline__ void reset_env(const EnvConst& c, const EnvState& s, int
 //   n_hist: entries in the demand-history deque (0 at reset)
 //   shh/sht: per-lane LDS shipped-home / shipped-total of this step (null at reset)
 // ------------------------------------------------------------------------------------------
-//   pipe   : per-lane LDS scratch of Lmax*K ints ([l*K + sku] * BS), the pipeline buckets
+//   shh/sht are indexed [(w * K + sku) * BS] from a pointer already offset to the env's column.
+// One agent (warehouse w) per call: the step kernel builds the W agents of an env in parallel.
 template <int K>
-__device__ __noinline__ void build_obs(const EnvConst& c, const EnvState& s, int64_t e, int t_now, int n_hist,
-                                       const int32_t* shh, const int32_t* sht, int32_t* pipe, float* out) {
+__device__ __noinline__ void build_obs_agent(const EnvConst& c, const EnvState& s, int64_t e, int w, int t_now,
+                                             int n_hist, const int32_t* shh, const int32_t* sht, float* out) {
   const int64_t E = c.E;
   const int W = c.W, RING = c.RING, Lmax = c.Lmax;
   const uint32_t f = c.flags;
   const bool ratio = c.norm == MSC_OBS_RATIO, meanstd = c.norm == MSC_OBS_MEANSTD;
   const double eps = 1e-8;
   const float epsf = 1e-8f;
-  for (int w = 0; w < W; w++) {
+  {
     float* o = out + (int64_t)w * c.L;
     int j = 0;  // feature index (excludes the one-hot)
     auto put = [&](double v) {
@@ -225,28 +226,30 @@ __device__ __noinline__ void build_obs(const EnvConst& c, const EnvState& s, int
       rm[sk] = n_hist > 0 ? (float)hs / (float)n_hist : 0.0f;
       pend_sum[sk] = 0;
     }
-    // pipeline bucket of each pending order (one pass over the ring): expected arrival - t_now,
-    // overdue orders into slot 0 (_compute_pipeline, multi_env.py:956-966)
-    for (int l = 0; l < Lmax * K; l++) pipe[l * BS] = 0;
+    // pipeline buckets (_compute_pipeline, multi_env.py:956-966): an order of age a (ring slot
+    // (t_now - a) mod RING) expects to arrive in elt - a steps and lands in bucket
+    // max(1, elt - a) - 1, so bucket l >= 1 holds exactly the order of age elt - 1 - l and bucket 0
+    // every order of age >= elt - 1 (due next step or overdue). Read straight from the ring.
     int pend_total = 0;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
-      const int i = w * K + sk;
-      const int elt = c.elt[i];
-      const int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
-      for (int jr = 0; jr < RING; jr++) {
-        const int q = rq[jr * E];
-        if (q == 0) continue;
-        int age = (t_now - jr) % RING;
-        if (age < 0) age += RING;
-        int slot = elt - age;
-        slot = slot < 1 ? 1 : slot;
-        pipe[((slot - 1) * K + sk) * BS] += q;
-        pend_sum[sk] += q;
-      }
+      const int32_t* rq = s.ring_q + (int64_t)(w * K + sk) * RING * E + e;
+      for (int jr = 0; jr < RING; jr++) pend_sum[sk] += rq[jr * E];
       pend_total += pend_sum[sk];
     }
-    auto pipe_at = [&](int l, int sk) -> int { return pipe[(l * K + sk) * BS]; };
+    auto pipe_at = [&](int l, int sk) -> int {
+      const int elt = c.elt[w * K + sk];
+      const int32_t* rq = s.ring_q + (int64_t)(w * K + sk) * RING * E + e;
+      auto at_age = [&](int a) -> int {
+        int jr = (t_now - a) % RING;
+        if (jr < 0) jr += RING;
+        return rq[jr * E];
+      };
+      if (l > 0) return l + 1 <= elt ? at_age(elt - 1 - l) : 0;
+      int v = 0;
+      for (int a = elt - 1 > 0 ? elt - 1 : 0; a < RING; a++) v += at_age(a);
+      return v;
+    };
     double inv_total = 0.0, shipped_total = 0.0, sa_total = 0.0;
     float dh_total = 0.0f;
 #pragma unroll
@@ -352,6 +355,13 @@ __device__ __noinline__ void build_obs(const EnvConst& c, const EnvState& s, int
   }
 }
 
+// all W agents of env e (reset path: one lane per env)
+template <int K>
+__device__ __forceinline__ void build_obs(const EnvConst& c, const EnvState& s, int64_t e, int t_now, int n_hist,
+                                          const int32_t* shh, const int32_t* sht, float* out) {
+  for (int w = 0; w < c.W; w++) build_obs_agent<K>(c, s, e, w, t_now, n_hist, shh, sht, out);
+}
+
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
@@ -360,12 +370,11 @@ __global__ __launch_bounds__(BS) void reset_kernel(const DevEnv* __restrict__ dp
                                                    const uint32_t* new_roots, int32_t flags, float* obs) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
-  extern __shared__ __attribute__((aligned(16))) int32_t lds[];  // [Lmax*K][BS] pipeline scratch
   const int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x;
   if (e >= c.E) return;
   if (mask && !mask[e]) return;
   reset_env<K>(c, s, e, flags, new_roots ? new_roots + e : nullptr);
-  if (obs) build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, lds + threadIdx.x, obs + e * c.W * c.L);
+  if (obs) build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, obs + e * c.W * c.L);
 }
 
 // PoissonDemandSampler.sample (demand_sampler.py:105-163), production version: a flat per-lane
@@ -1153,7 +1162,6 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
   int32_t* Lqsr = lds + 1 * WK * BS + lane;   // [WK]  shipped to the current region
   int32_t* Lsht = lds + 2 * WK * BS + lane;   // [WK]  shipped in total this step
   int32_t* Lshh = lds + 3 * WK * BS + lane;   // [WK]  shipped to the home region
-  int32_t* Lpipe = lds + 4 * WK * BS + lane;  // [Lmax*K] pipeline buckets (observations)
   double* Lpen = reinterpret_cast<double*>(lds + ni) + lane;  // [W] penalty cost
   double* Lout = Lpen + W * BS;                                // [W] outbound cost
   double* Linb = Lout + W * BS;                                // [W] inbound cost
@@ -1633,11 +1641,11 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
   const int64_t obs_off = e * W * c.L;
   if (!trunc) {
     s.t[e] = t + 1;
-    if (!(c.ablate & 1)) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, Lpipe, io.obs + obs_off);
+    if (!(c.ablate & 1)) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, io.obs + obs_off);
   } else {
-    if (io.final_obs) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, Lpipe, io.final_obs + obs_off);
+    if (io.final_obs) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, io.final_obs + obs_off);
     reset_env<K>(c, s, e, 0, nullptr);
-    build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, Lpipe, io.obs + obs_off);
+    build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, io.obs + obs_off);
   }
 }
 
@@ -1676,8 +1684,7 @@ static dim3 grid_for(int64_t E, int epw = BS) { return dim3((unsigned)((E + epw 
 
 hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask, const uint32_t* new_roots,
                         int32_t flags, float* obs, hipStream_t st) {
-  const size_t lds = (size_t)c.Lmax * c.K * BS * sizeof(int32_t);
-  MSC_K_SWITCH(c.K, hipLaunchKernelGGL(reset_kernel<K>, grid_for(c.E), dim3(BS), lds, st, d, mask, new_roots, flags, obs));
+  MSC_K_SWITCH(c.K, hipLaunchKernelGGL(reset_kernel<K>, grid_for(c.E), dim3(BS), 0, st, d, mask, new_roots, flags, obs));
   return hipGetLastError();
 }
 
