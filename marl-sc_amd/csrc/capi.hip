@@ -232,6 +232,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     const char* pm = getenv("MSC_PARK_MIN");
     c.park_min = pm && atoi(pm) >= 1 && atoi(pm) <= 64 ? atoi(pm) : 32;
     c.epw_step = epw("MSC_STEP_EPW", 64);
+    const char* si = getenv("MSC_STEP_IMPL");
+    c.step_impl = si && strcmp(si, "lane") == 0 ? 1 : 0;
   }
 
   TablePack tp;
@@ -327,6 +329,11 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   const size_t a_root = slot(sizeof(uint32_t) * E);
   const size_t a_emp = slot(sizeof(int32_t) * E);
   const size_t a_err = slot(sizeof(uint32_t) * 4);
+  const size_t a_sht = slot(sizeof(int32_t) * WK * E);
+  const size_t a_shh = slot(sizeof(int32_t) * WK * E);
+  const size_t a_pen = slot(sizeof(double) * W * E);
+  const size_t a_out = slot(sizeof(double) * W * E);
+  const size_t a_inb = slot(sizeof(double) * W * E);
   env->arena_bytes = off;
   if (hipMalloc(&env->arena, off) != hipSuccess) return fail(set_err(-2, "hipMalloc(state arena, %zu B) failed", off));
   if (hipMemset(env->arena, 0, off) != hipSuccess) return fail(set_err(-2, "memset arena failed"));
@@ -348,6 +355,11 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   s.root = (uint32_t*)(ab + a_root);
   s.emp_start = (int32_t*)(ab + a_emp);
   s.err = (uint32_t*)(ab + a_err);
+  s.sc_sht = (int32_t*)(ab + a_sht);
+  s.sc_shh = (int32_t*)(ab + a_shh);
+  s.sc_pen = (double*)(ab + a_pen);
+  s.sc_out = (double*)(ab + a_out);
+  s.sc_inb = (double*)(ab + a_inb);
   EnvState s2 = s;
   if (d->demand_type == MSC_DEMAND_POISSON) {
     const size_t rec_bytes = sizeof(uint4) * (size_t)nv * order_cap * E;

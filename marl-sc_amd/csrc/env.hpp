@@ -35,7 +35,8 @@ struct EnvConst {
   int32_t demand_gen;   // generator waves per block of the split demand kernel (1 or 2)
   int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
-  int32_t epw_step;     // envs per 64-lane block of the step kernel
+  int32_t epw_step;     // envs per 64-lane block of the lane-per-env step kernel (A/B only)
+  int32_t step_impl;    // 0 = group-per-env step kernel (default), 1 = lane-per-env (MSC_STEP_IMPL=lane)
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;
@@ -80,6 +81,13 @@ struct EnvState {
   MSC_G int32_t* emp_start;  // [E] EmpiricalDemandSampler window start row (-1: not drawn)
   uint4* orders;       // [order_cap][E][NV] per-step order records (Poisson sampler output)
   MSC_G int32_t* n_orders;   // [E]
+  // step phase scratch (step_a/b/c kernels): shipped total / home [WK][E], penalty / outbound /
+  // inbound cost [W][E]
+  MSC_G int32_t* sc_sht;
+  MSC_G int32_t* sc_shh;
+  MSC_G double* sc_pen;
+  MSC_G double* sc_out;
+  MSC_G double* sc_inb;
   MSC_G uint32_t* err;       // [1] device error bits
 };
 

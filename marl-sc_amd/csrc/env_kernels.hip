@@ -193,7 +193,8 @@ __device__ __noinline__ void reset_env(const EnvConst& c, const EnvState& s, int
 // One agent (warehouse w) per call: the step kernel builds the W agents of an env in parallel.
 template <int K>
 __device__ __noinline__ void build_obs_agent(const EnvConst& c, const EnvState& s, int64_t e, int w, int t_now,
-                                             int n_hist, const int32_t* shh, const int32_t* sht, float* out) {
+                                             int n_hist, const int32_t* shh, const int32_t* sht, int64_t sstride,
+                                             float* out) {
   const int64_t E = c.E;
   const int W = c.W, RING = c.RING, Lmax = c.Lmax;
   const uint32_t f = c.flags;
@@ -218,8 +219,8 @@ __device__ __noinline__ void build_obs_agent(const EnvConst& c, const EnvState& 
       const int i = w * K + sk;
       inv[sk] = s.inv[i * E + e];
       dh[sk] = s.inc[i * E + e];
-      sh[sk] = shh ? shh[i * BS] : 0;
-      sa[sk] = sht ? sht[i * BS] - sh[sk] : 0;
+      sh[sk] = shh ? shh[i * sstride] : 0;
+      sa[sk] = sht ? sht[i * sstride] - sh[sk] : 0;
       fc[sk] = s.fc[i * E + e];
       int hs = 0;
       for (int h = 0; h < n_hist; h++) hs += s.hist[(((t_now - n_hist + 1 + h) % MSC_HISTORY) * W * K + i) * E + e];
@@ -359,7 +360,7 @@ __device__ __noinline__ void build_obs_agent(const EnvConst& c, const EnvState& 
 template <int K>
 __device__ __forceinline__ void build_obs(const EnvConst& c, const EnvState& s, int64_t e, int t_now, int n_hist,
                                           const int32_t* shh, const int32_t* sht, float* out) {
-  for (int w = 0; w < c.W; w++) build_obs_agent<K>(c, s, e, w, t_now, n_hist, shh, sht, out);
+  for (int w = 0; w < c.W; w++) build_obs_agent<K>(c, s, e, w, t_now, n_hist, shh, sht, BS, out);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1649,6 +1650,474 @@ __global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp,
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Production step: InventoryEnvironment.step (multi_env.py:253-366) as three launches.
+//
+//   step_a_kernel  (block = 64 envs x W waves; wave = warehouse, lane = env): per-env RNG work
+//                  (stochastic lead deviations, empirical window), then orders / lead times /
+//                  pending ring / arrivals / inbound cost for the lane's (w, s) pairs;
+//   step_b_kernel  (group of GW >= W lanes = one env, lane = warehouse): the greedy allocation.
+//                  Each lane keeps its warehouse's inventory / shipped-to-region / shipped-total /
+//                  shipped-home in registers and computes its own ranking cost; the group finds the
+//                  cheapest candidate with a butterfly (lowest index on ties = the stable argsort),
+//                  and the region epilogue (lost sales, home features) is per-warehouse lane work;
+//   step_c_kernel  (wave = warehouse, lane = env): inventory / history / forecast, rewards (team
+//                  sum across the block's waves), observations, in-kernel reset on truncation.
+// Splitting keeps each kernel's register footprint small (the fused version spilled) and gives
+// every phase its own natural thread mapping; the phases exchange ~0.7 KB per env through HBM
+// scratch (EnvState::sc_*), and [i][E] state stays coalesced for the wave = warehouse phases.
+// ------------------------------------------------------------------------------------------
+// numpy pairwise sum (add.reduce, n <= 16): sequential below 8 elements, else 8 accumulators
+// (static indices only: v stays in registers)
+__device__ __forceinline__ double np_sum_f64_16(const double (&v)[16], int n) {
+  if (n < 8) {
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r = i < n ? r + v[i] : r;
+    return r;
+  }
+  double a[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) a[j] = n >= 16 ? v[j] + v[8 + j] : v[j];
+  double r = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+  for (int i = 8; i < 16; i++) r = (n < 16 && i < n) ? r + v[i] : r;
+  return r;
+}
+
+// ---- phase A ------------------------------------------------------------------------------
+template <int K, bool DBG>
+__global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  extern __shared__ __attribute__((aligned(16))) int32_t Ldev[];  // stochastic: [w*K+s][lane] deviations
+  __shared__ int32_t Lt[BS];
+  const int W = c.W, WK = W * K, RING = c.RING;
+  const int64_t E = c.E;
+  const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;
+  const int64_t e = (int64_t)blockIdx.x * BS + lane;
+  const bool ev = e < E;
+  const msc_step_info info = io.info;
+  constexpr bool dbg = DBG;
+  const bool stoch = c.lead_type == MSC_LEAD_STOCHASTIC;
+  if (wave == 0 && ev) {  // per-env sequential RNG work
+    const int t = s.t[e];
+    Lt[lane] = t;
+    if (stoch) {  // lead_time_sampler.sample(): all W*K deviations every step (multi_env.py:866)
+      Pcg64 rl = load_rng(s, 1, e, E);
+      if (c.dev_per_sku) {  // SKU-major column_stack order (lead_time_sampler.py:181-185)
+        for (int sk = 0; sk < K; sk++)
+          for (int w = 0; w < W; w++)
+            Ldev[(w * K + sk) * BS + lane] = (int32_t)bounded_int(rl, -c.maxdev[sk], (int64_t)c.maxdev[sk] + 1);
+      } else {
+        for (int i = 0; i < WK; i++) Ldev[i * BS + lane] = (int32_t)bounded_int(rl, -c.maxdev[0], (int64_t)c.maxdev[0] + 1);
+      }
+      store_rng(s, 1, e, E, rl);
+    }
+    if (c.demand_type == MSC_DEMAND_EMPIRICAL && s.emp_start[e] < 0) {  // demand_sampler.py:227-241
+      Pcg64 rg = load_rng(s, 0, e, E);
+      s.emp_start[e] = (int)bounded_int(rg, 0, (int64_t)(c.tr_rows - c.T) + 1);
+      store_rng(s, 0, e, E, rg);
+    }
+  }
+  __syncthreads();
+  if (wave >= W || !ev) return;
+  const int w = wave, t = Lt[lane];
+  const int slot = t % RING;
+  double inbF = 0.0, inbV = 0.0;
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) {
+    const int i = w * K + sk;
+    const float a = io.actions[(e * W + w) * K + sk];
+    const int inc_old = s.inc[i * E + e];
+    int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
+    int pend = 0;
+    for (int jr = 0; jr < RING; jr++) pend += rq[jr * E];
+    const double prm = c.act_param[sk];  // _rescale_actions_to_quantities (multi_env.py:795-848)
+    double q;
+    if (c.action_type == MSC_ACTION_DIRECT) {
+      q = rint((double)((a + 1.0f) / 2.0f) * prm);
+      q = q < 0.0 ? 0.0 : (q > prm ? prm : q);
+    } else if (c.action_type == MSC_ACTION_DEMAND_CENTERED) {
+      q = rint(prm * (double)a) + (double)inc_old;
+      q = q < 0.0 ? 0.0 : q;
+    } else {
+      const double target = (double)((a + 1.0f) / 2.0f) * prm;
+      q = rint((target - (double)(float)inc_old) - (double)(float)pend);
+      q = q < 0.0 ? 0.0 : q;
+    }
+    const int qi = (int)q;
+    const int elt = c.elt[i];
+    int lact = elt;
+    if (stoch) {
+      lact = elt + Ldev[i * BS + lane];
+      lact = lact > 1 ? lact : 1;
+    }
+    rq[slot * E] = qi;  // _apply_orders: the slot of order time t
+    if (stoch) s.ring_l[((int64_t)i * RING + slot) * E + e] = (uint8_t)lact;
+    int inv = s.inv[i * E + e];  // _apply_arrivals: actual arrival == t
+    if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = inv;
+    for (int jr = 0; jr < RING; jr++) {
+      if (jr == slot) continue;
+      const int qq = rq[jr * E];
+      if (qq == 0) continue;
+      int age = (t - jr) % RING;
+      if (age < 0) age += RING;
+      const int l = stoch ? (int)s.ring_l[((int64_t)i * RING + jr) * E + e] : elt;
+      if (l == age) {
+        inv += qq;
+        rq[jr * E] = 0;
+      }
+    }
+    s.inv[i * E + e] = inv;
+    s.inc[i * E + e] = 0;
+    if (qi > 0) inbF += c.inF[i];
+    inbV += ((double)qi * c.skw[sk]) * c.inV[i];
+    if (dbg) {
+      if (info.pending_total) info.pending_total[e * WK + i] = pend;
+      if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
+    }
+  }
+  s.sc_inb[w * E + e] = inbF + inbV;
+}
+
+// ---- phase B ------------------------------------------------------------------------------
+// Butterfly partner exchange inside a group of GW lanes with DPP (a VALU operand modifier, no LDS
+// round trip): step 0 pairs lanes i ^ 1 and step 1 lanes i ^ 2 (quad_perm), step 2 the two quads
+// of an 8-lane row half (row_half_mirror), step 3 the two halves of a 16-lane row (row_mirror).
+// Every step pairs lanes whose partial results cover disjoint halves, so min / sum reductions end
+// with the group result in every lane.
+template <int S>
+__device__ __forceinline__ int dpp_x(int v) {
+  constexpr int ctrl = S == 0 ? 0xB1 : S == 1 ? 0x4E : S == 2 ? 0x141 : 0x140;
+  return __builtin_amdgcn_update_dpp(0, v, ctrl, 0xF, 0xF, false);
+}
+template <int S>
+__device__ __forceinline__ double dpp_x(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_x<S>((int)(b & 0xffffffffLL)), hi = dpp_x<S>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int GW, typename T, typename F>
+__device__ __forceinline__ T group_reduce(T v, F op) {
+  v = op(v, dpp_x<0>(v));
+  if constexpr (GW >= 4) v = op(v, dpp_x<1>(v));
+  if constexpr (GW >= 8) v = op(v, dpp_x<2>(v));
+  if constexpr (GW >= 16) v = op(v, dpp_x<3>(v));
+  return v;
+}
+
+template <int K, int GW, bool DBG>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  const int W = c.W, WK = W * K, R = c.R;
+  const int64_t E = c.E;
+  const int w = threadIdx.x % GW;
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GW;
+  const bool ev = e < E, wl = w < W;
+  const msc_step_info info = io.info;
+  constexpr bool dbg = DBG;
+  int inv[K], qsr[K], sht[K], shh[K];
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) {
+    inv[sk] = (ev && wl) ? s.inv[(int64_t)(w * K + sk) * E + e] : 0;
+    qsr[sk] = sht[sk] = shh[sk] = 0;
+  }
+  double pen = 0.0, out = 0.0, cof = 0.0, cov = 0.0;
+  int n_orders = 0;
+  const MSC_GLOBAL uint4* src;
+  int64_t stride;
+  if (c.demand_type == MSC_DEMAND_EMPIRICAL) {
+    int64_t off = 0;
+    if (ev) {
+      const int64_t row = s.emp_start[e] + (s.t[e] % c.T);
+      off = c.tr_off[row];
+      n_orders = (int)(c.tr_off[row + 1] - off);
+    }
+    src = gp(c.tr_rec + off * Rec<K>::NV);
+    stride = 1;
+  } else {
+    n_orders = ev ? s.n_orders[e] : 0;
+    src = gp(s.orders + (ev ? e : 0));
+    stride = E;
+  }
+  if (dbg && ev && w == 0 && info.n_orders) info.n_orders[e] = n_orders;
+  constexpr int NVR = Rec<K>::NV;
+  const int64_t rec_step = stride * NVR;
+  const int maxwh = c.max_wh;
+  int cur = -1, lost_cnt = 0;
+  int u[K], dsum[K];
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
+
+  // region epilogue: lost sales (lost_sales_handler.py) into the penalty cost, home-region
+  // features, per-region infos; every lane handles its own warehouse
+  auto finalize = [&](int r) {
+    if (lost_cnt > 0) {
+      double upen = 0.0;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++)
+        upen += c.pen_per_sku ? (double)u[sk] * c.pen[sk] : ((double)u[sk] * c.skw[sk]) * c.pen_scalar;
+      double wt = 0.0;  // this warehouse's share of the region's lost sales
+      if (c.lost_type == MSC_LOST_CLOSEST) {
+        wt = (wl && w == c.closest[r]) ? 1.0 : 0.0;
+      } else if (c.lost_type == MSC_LOST_SHIPMENT) {
+        int acc = 0;
+#pragma unroll
+        for (int sk = 0; sk < K; sk++) acc += qsr[sk];
+        const double qr = wl ? (double)acc : 0.0;
+        // integer-valued: exact in any summation order
+        const double tot = group_reduce<GW>(qr, [](double a, double b) { return a + b; });
+        if (tot > 0.0) wt = qr > 0.0 ? qr / tot : 0.0;
+        else wt = (wl && w == c.closest[r]) ? 1.0 : 0.0;
+      } else {  // cost: softmax(-(of * lost_orders + ov * lost_weight) / alpha), numpy sum order
+        double lw = 0.0;
+#pragma unroll
+        for (int sk = 0; sk < K; sk++) lw += (double)u[sk] * c.skw[sk];
+        const double lg = wl ? -(cof * (double)lost_cnt + cov * lw) / c.alpha : -INFINITY;
+        const double mx = group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
+        const double ex = wl ? exp(lg - mx) : 0.0;
+        double all[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) all[j] = j < GW ? __shfl(ex, j, GW) : 0.0;
+        wt = wl ? ex / np_sum_f64_16(all, W) : 0.0;
+      }
+      // (a closest-warehouse share is 1.0 and 1.0 * x == x: one update form serves every type)
+      if (wt != 0.0) {
+        pen += wt * upen;
+        if (dbg && info.lost_sales)
+#pragma unroll
+          for (int sk = 0; sk < K; sk++) info.lost_sales[e * WK + w * K + sk] += wt * (double)u[sk];
+      }
+    }
+    // home-region features: incoming demand and units shipped home (multi_env.py:767-773)
+    if (wl && (c.home_mask[r] >> w & 1u)) {
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {
+        s.inc[(int64_t)(w * K + sk) * E + e] = dsum[sk];
+        shh[sk] = qsr[sk];
+      }
+    }
+    if (dbg && w == 0) {
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {
+        if (info.demand_per_region) info.demand_per_region[(e * R + r) * K + sk] = dsum[sk];
+        if (info.unfulfilled_demands) info.unfulfilled_demands[(e * R + r) * K + sk] = u[sk];
+      }
+      if (info.lost_order_counts) info.lost_order_counts[e * R + r] = lost_cnt;
+    }
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) qsr[sk] = 0;
+  };
+
+  constexpr int PF = 4;
+  uint4 ring[PF][NVR];
+#pragma unroll
+  for (int q = 0; q < PF; q++)
+#pragma unroll
+    for (int j = 0; j < NVR; j++) ring[q][j] = (q < n_orders) ? gload4(src, q * rec_step + j * stride) : make_uint4(0, 0, 0, 0);
+  for (int oi = 0; oi <= n_orders; oi++) {
+    int r = -1;
+    int d[K];
+    {
+      union {
+        uint4 v[NVR];
+        uint16_t h[8 * NVR];
+      } ur;
+#pragma unroll
+      for (int j = 0; j < NVR; j++) ur.v[j] = ring[0][j];
+      if (oi < n_orders) r = ur.h[0];
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
+    }
+#pragma unroll
+    for (int q = 0; q + 1 < PF; q++)
+#pragma unroll
+      for (int j = 0; j < NVR; j++) ring[q][j] = ring[q + 1][j];
+    if (oi + PF < n_orders) {
+#pragma unroll
+      for (int j = 0; j < NVR; j++) ring[PF - 1][j] = gload4(src, (oi + PF) * rec_step + j * stride);
+    }
+    if (r != cur) {
+      if (cur >= 0) finalize(cur);
+      if (r >= 0 && wl) {
+        cof = c.ofT[r * W + w];
+        cov = c.ovT[r * W + w];
+      }
+      cur = r;
+      lost_cnt = 0;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
+    }
+    if (oi == n_orders) break;
+    bool any_d = false;
+    double tw = 0.0;
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      dsum[sk] += d[sk];
+      any_d |= d[sk] > 0;
+      tw += (double)d[sk] * c.skw[sk];
+    }
+    if (!any_d) continue;  // an empty order ships nothing and is never lost
+    int rem[K];
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
+    const double mycost = cof + cov * tw;  // demand_allocator.py:168-172
+    bool used_me = false;
+    int used = 0;
+    bool open = true;
+    while (open) {
+      bool has = false;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) has |= rem[sk] > 0 && inv[sk] > 0;
+      double bc = (has && wl && !used_me) ? mycost : INFINITY;
+      int bw = w;
+      auto amin = [&](auto step) {  // group argmin, lowest warehouse on ties
+        const double oc = step(bc);
+        const int ow = step(bw);
+        const bool take = oc < bc || (oc == bc && ow < bw);
+        bc = take ? oc : bc;
+        bw = take ? ow : bw;
+      };
+      amin([](auto v) { return dpp_x<0>(v); });
+      if constexpr (GW >= 4) amin([](auto v) { return dpp_x<1>(v); });
+      if constexpr (GW >= 8) amin([](auto v) { return dpp_x<2>(v); });
+      if constexpr (GW >= 16) amin([](auto v) { return dpp_x<3>(v); });
+      if (bc == INFINITY) break;  // nobody holds a still-needed SKU
+      const bool me = w == bw;
+      int fl[K];
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) fl[sk] = me ? (rem[sk] < inv[sk] ? rem[sk] : inv[sk]) : 0;
+      bool done = true;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {  // the winner's fill reaches every lane as a group sum
+        rem[sk] -= group_reduce<GW>(fl[sk], [](int a, int b) { return a + b; });
+        done &= rem[sk] <= 0;
+      }
+      if (me) {
+        double fw = 0.0;
+        int fsum = 0;
+#pragma unroll
+        for (int sk = 0; sk < K; sk++) {
+          inv[sk] -= fl[sk];
+          qsr[sk] += fl[sk];
+          sht[sk] += fl[sk];
+          fsum += fl[sk];
+          fw += (double)fl[sk] * c.skw[sk];
+        }
+        out += fw == tw ? bc : cof + cov * fw;  // whole order from here: the ranking cost bit for bit
+        used_me = true;
+        if (dbg) {
+#pragma unroll
+          for (int sk = 0; sk < K; sk++) {
+            if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] += fl[sk];
+            if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
+          }
+          if (info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] += 1;
+          if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] += fsum;
+        }
+      }
+      used++;
+      open = !done && used < maxwh;
+    }
+    bool anyrem = false;
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      anyrem |= rem[sk] > 0;
+      u[sk] += rem[sk] > 0 ? rem[sk] : 0;
+    }
+    lost_cnt += anyrem ? 1 : 0;
+  }
+  if (ev && wl) {
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int64_t i = (int64_t)(w * K + sk) * E + e;
+      s.inv[i] = inv[sk];
+      s.sc_sht[i] = sht[sk];
+      s.sc_shh[i] = shh[sk];
+    }
+    s.sc_pen[w * E + e] = pen;
+    s.sc_out[w * E + e] = out;
+  }
+}
+
+// ---- phase C ------------------------------------------------------------------------------
+template <int K, bool DBG>
+__global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  extern __shared__ __attribute__((aligned(16))) double Lrw[];  // [W][BS] rewards (team sum)
+  const int W = c.W, WK = W * K;
+  const int64_t E = c.E;
+  const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;
+  const int64_t e = (int64_t)blockIdx.x * BS + lane;
+  const bool act = wave < W && e < E;
+  const int w = wave;
+  const msc_step_info info = io.info;
+  constexpr bool dbg = DBG;
+  int t = 0;
+  double rw = 0.0;
+  if (act) {
+    t = s.t[e];
+    const int hslot = t % MSC_HISTORY;
+    double hold = 0.0;
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      const int iv = s.inv[i * E + e];
+      const int v = s.inc[i * E + e];
+      s.hist[((int64_t)hslot * WK + i) * E + e] = v;
+      s.fc[i * E + e] = 0.3f * (float)v + 0.7f * s.fc[i * E + e];  // EMA forecast (f32)
+      hold += c.hold_per_sku ? (double)iv * c.hold[sk] : ((double)iv * c.skw[sk]) * c.hold_scalar;
+    }
+    const double pen = s.sc_pen[w * E + e], out = s.sc_out[w * E + e], inb = s.sc_inb[w * E + e];
+    rw = -((((hold + pen) + out) + inb) * c.scale);
+    Lrw[w * BS + lane] = rw;
+    if (dbg && info.costs) {
+      info.costs[(e * 4 + 0) * W + w] = hold;
+      info.costs[(e * 4 + 1) * W + w] = pen;
+      info.costs[(e * 4 + 2) * W + w] = out;
+      info.costs[(e * 4 + 3) * W + w] = inb;
+    }
+  }
+  __syncthreads();
+  bool trunc = false;
+  const int64_t obs_off = e * W * c.L;
+  // shipped home / total of this step, [(w*K+s) * E] from the env's column
+  const int32_t* shh = s.sc_shh + e;
+  const int32_t* sht = s.sc_sht + e;
+  if (act) {
+    double v = rw;
+    if (c.scope == MSC_SCOPE_TEAM) {  // team scope: sum over agents in agent order
+      v = 0.0;
+      for (int j = 0; j < W; j++) v += Lrw[j * BS + lane];
+    }
+    io.rew[e * W + w] = (float)v;
+    if (io.rew64) io.rew64[e * W + w] = v;
+    const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
+    trunc = t + 1 >= c.T;
+    if (!trunc) {
+      if (!(c.ablate & 1)) build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.obs + obs_off);
+    } else if (io.final_obs) {
+      build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
+    }
+  }
+  // truncation: reset the env (one sequential RNG pass per env), then every agent's reset obs
+  if (__syncthreads_or(trunc ? 1 : 0)) {
+    if (act && w == 0) {
+      io.trunc[e] = trunc ? 1 : 0;
+      if (trunc) reset_env<K>(c, s, e, 0, nullptr);
+      else s.t[e] = t + 1;
+    }
+    __syncthreads();
+    if (act && trunc) build_obs_agent<K>(c, s, e, w, 0, 0, nullptr, nullptr, 0, io.obs + obs_off);
+  } else if (act && w == 0) {
+    io.trunc[e] = 0;
+    s.t[e] = t + 1;
+  }
+}
+
 // flat per-agent obs [E][W][L(1+W)] = local_w || local_0 .. local_{W-1} (multi_env.py:566-573)
 __global__ void obs_flat_kernel(const float* __restrict__ obs, float* __restrict__ flat, int64_t E, int W, int L) {
   const int64_t FL = (int64_t)L * (1 + W);
@@ -1735,6 +2204,24 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
   const size_t lds = step_lds_bytes(c);
   if (gen && c.demand_type == MSC_DEMAND_POISSON) launch_demand_k<K>(c, d, st);
   using KFn = void (*)(const DevEnv*, StepIO);
+  if (c.step_impl == 0) {  // production: three phase kernels, group-per-env allocation
+    const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : c.W <= 8 ? 8 : 16;
+    const bool dbg = io.has_info != 0;  // collect_step_info: the instrumented instantiations
+    KFn a = dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>;
+    KFn cc = dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>;
+    KFn b;
+    if (dbg)
+      b = GW == 2 ? (KFn)step_b_kernel<K, 2, true> : GW == 4 ? (KFn)step_b_kernel<K, 4, true>
+        : GW == 8 ? (KFn)step_b_kernel<K, 8, true> : (KFn)step_b_kernel<K, 16, true>;
+    else
+      b = GW == 2 ? (KFn)step_b_kernel<K, 2, false> : GW == 4 ? (KFn)step_b_kernel<K, 4, false>
+        : GW == 8 ? (KFn)step_b_kernel<K, 8, false> : (KFn)step_b_kernel<K, 16, false>;
+    const size_t lds_a = c.lead_type == MSC_LEAD_STOCHASTIC ? (size_t)c.W * K * BS * sizeof(int32_t) : 0;
+    hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * c.W), lds_a, st, d, io);
+    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), 0, st, d, io);
+    hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), (size_t)c.W * BS * sizeof(double), st, d, io);
+    return hipGetLastError();
+  }
   const bool t = c.cost_lds != 0;
   KFn fn;
   if (c.W <= 4) fn = t ? (KFn)step_kernel<K, 4, true> : (KFn)step_kernel<K, 4, false>;
