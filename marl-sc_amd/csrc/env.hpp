@@ -31,8 +31,8 @@ struct EnvConst {
   int32_t cost_lds;     // 1: step kernel stages the [R][W] outbound cost tables in LDS
   int32_t dem_lds;      // 1: demand kernel stages the Poisson rate tables in LDS
   int32_t ablate;       // timing-only phase ablation bits (MSC_ABLATE env var); 0 in production
-  int32_t demand_impl;  // 0 = generator/parser split (default); A/B only: 1 nested, 2 flat_branchy, 3 flat
-  int32_t demand_gen;   // generator waves per block of the split demand kernel (1 or 2)
+  int32_t demand_impl;  // 0 = generator waves + unit-per-round parser (default); A/B: 1 nested, 2 flat_branchy, 3 flat, 4 park1, 5 park4
+  int32_t demand_gen;   // generator waves per block of the split demand kernel (1, 2 or 3)
   int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
   int32_t epw_step;     // envs per 64-lane block of the lane-per-env step kernel (A/B only)

@@ -950,6 +950,243 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_park4_kernel(const DevEnv
   s.n_orders[e] = n;
 }
 
+// ------------------------------------------------------------------------------------------
+// demand_unit_kernel: converged "one unit per round" parser (production default).
+//
+// Same generator waves as the parking kernels, but the parser no longer parks lanes: in every
+// round EVERY live lane runs its current unit over the next UD = 8 uniforms at once and settles
+// it in the same round. A Poisson unit (a region's order count or one SKU quantity) chains the
+// UD products p_i = p_{i-1} * U_i (the reference's `prod *= U` in order, bit-exact), compares
+// each against exp(-lambda) and takes the leading run of continues plus the ending draw; the
+// rare unit that is still going after UD draws (X >= UD) carries its product into the next
+// round. A mask unit compares min(UD, K - k) uniforms against the folded Bernoulli threshold.
+// With no park check, no ballot and no lane-mask logic the round is straight-line code, and a
+// wave runs for ~ max over its lanes of (units + overflow segments) ~ 1.4k rounds at 8x64x5
+// instead of ~3k hot steps + ~1.5k settle passes of demand_park4_kernel.
+// Ring: lane-major [64][USTR], slot = position mod UCAP; slots 0..UD-2 are mirrored at UCAP..
+// so the UD reads of a round are one base address + immediate offsets (no wrap arithmetic).
+// ------------------------------------------------------------------------------------------
+constexpr int UD = 8;                       // uniforms per round
+constexpr int UHS = 4;                      // rounds per chunk (<= UD * UHS draws per lane)
+constexpr int UCAP = 2 * UD * UHS;          // ring capacity (positions)
+constexpr int USTR = UCAP + UD - 1;         // lane stride in doubles (odd: conflict-free b64 reads)
+static_assert((UCAP & (UCAP - 1)) == 0 && (USTR & 1) == 1, "ring layout");
+
+__host__ __device__ constexpr size_t unit_lds_fixed() {
+  return (size_t)BS * USTR * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
+}
+
+template <int K, int G, bool LDS_TAB>
+__global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv* __restrict__ dp) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  const int R = c.R;
+  constexpr int NV = Rec<K>::NV;
+  constexpr int NW = 4 * NV;
+  extern __shared__ __attribute__((aligned(16))) double plds[];
+  __shared__ int more[2];
+  double* ring = plds;                                           // [BS][USTR]
+  int32_t* rdv = reinterpret_cast<int32_t*>(plds + BS * USTR);   // [2][BS]
+  const double* To = c.enlam_o;
+  const double* Tk = c.p_skip;
+  const double* Tq = c.enlam_q;
+  if constexpr (LDS_TAB) {
+    double* lo = plds + BS * USTR + BS;
+    double* lk = lo + R;
+    double* lq = lk + R;
+    for (int i = threadIdx.x; i < R; i += blockDim.x) {
+      lo[i] = c.enlam_o[i];
+      lk[i] = c.p_skip[i];
+    }
+    for (int i = threadIdx.x; i < R * K; i += blockDim.x) lq[i] = c.enlam_q[i];
+    To = lo;
+    Tk = lk;
+    Tq = lq;
+  }
+  const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;
+  const int64_t E = c.E;
+  const int64_t e = (int64_t)blockIdx.x * c.epw_dem + lane;
+  const bool valid = lane < c.epw_dem && e < E;
+  double* myring = ring + lane * USTR;
+
+  if (wave > 0) {
+    // ---------------- generator g: stream positions g, g + G, g + 2G, ...
+    const int g = wave - 1;
+    uint64_t th = 0, tl = 0, ih = 0, il = 1;
+    if (valid) {
+      Pcg64 rg = load_rng(s, 0, e, E);
+      for (int j = 0; j <= g; j++) pcg_step(rg);
+      th = rg.s_hi;
+      tl = rg.s_lo;
+      ih = rg.i_hi;
+      il = rg.i_lo;
+    }
+    uint64_t mh = PCG_MUL_HI, ml = PCG_MUL_LO, ch = ih, cl = il;
+    if constexpr (G > 1) pcg_jump_coeffs(G, ih, il, mh, ml, ch, cl);
+    int pg = g;
+    auto gen_to = [&](int target) {
+      while (pg < target) {
+        const double u = u64_to_double(pcg_output(th, tl));
+        const int slot = pg & (UCAP - 1);
+        myring[slot] = u;
+        if (slot < UD - 1) myring[slot + UCAP] = u;
+        uint64_t nh, nl;
+        mul128(th, tl, mh, ml, nh, nl);
+        add128(nh, nl, ch, cl);
+        th = nh;
+        tl = nl;
+        pg += G;
+      }
+    };
+    if (valid) gen_to(UCAP);
+    __syncthreads();
+    for (int ci = 0;; ci++) {
+      if (valid) gen_to(rdv[(ci & 1) * BS + lane] + UCAP);
+      __syncthreads();
+      if (!more[ci & 1]) break;
+    }
+    return;
+  }
+
+  // ---------------- parser
+  // Older and higher-priority waves win VALU issue arbitration on a SIMD (MI355X_MICROARCH.md,
+  // wave scheduling): the parser is the per-env critical path, the generators only need to stay
+  // a chunk ahead of it.
+  __builtin_amdgcn_s_setprio(2);
+  Pcg64 r0{};
+  if (valid) {
+    r0 = load_rng(s, 0, e, E);
+    store_rng_pre(s, e, E, r0);
+  }
+  rdv[lane] = 0;
+  static_assert(K <= UD, "a mask unit completes in one round");
+  int st = valid ? PS_ORD : PS_DONE, r = 0, x = 0, left = 0, sq = 0, n = 0, rd = 0;
+  unsigned mask = 0;
+  int mf = 0, live = valid ? 1 : 0, pend = 0;
+  const int cap = c.order_cap;
+  // the current order's record: written as {region, 0, ..., 0} when the order starts, then each
+  // SKU quantity is stored into its 16-bit field as its unit ends (same-lane stores to one
+  // address stay in program order)
+  const int64_t rstride = (int64_t)NV * E * 16;  // bytes between consecutive records of a lane
+  MSC_GLOBAL char* recp = reinterpret_cast<MSC_GLOBAL char*>(gp(s.orders + e)) - rstride;
+  __syncthreads();
+  // thresholds of the current region in registers (reloaded when a region starts, long before
+  // their first use): exp(-lambda_q[r, :]), p_skip[r], and exp(-lambda_o[r + 1])
+  double tq[K], tk = Tk[0], to_next = To[R > 1 ? 1 : 0];
+#pragma unroll
+  for (int j = 0; j < K; j++) tq[j] = Tq[j];
+  double prod = 1.0, thr = To[0];
+  // a unit ended: book its result, open the next unit (all lanes with a pending unit, predicated)
+  auto settle = [&]() {
+    const bool is_q = st == PS_QTY, is_o = st == PS_ORD;
+    if (is_q && n <= cap) {
+      const int h = 1 + sq;  // 16-bit field of the record (field 0 = region)
+      *reinterpret_cast<MSC_GLOBAL uint16_t*>(recp + (int64_t)(h >> 3) * E * 16 + (h & 7) * 2) =
+          (uint16_t)(x > 1 ? x : 1);  // max(1, Poisson(lambda_q))
+    }
+    mask = is_q ? (mask & (mask - 1u)) : mask;
+    left = is_o ? x : left;
+    const bool has_q = !is_o && mask != 0;
+    const int nsq = __builtin_ctz(mask | (1u << K));
+    // register select (the opaque copies keep the compiler from turning the chain back into an
+    // indexed load from a private array, i.e. scratch memory)
+    double q_thr = tq[0];
+#pragma unroll
+    for (int j = 1; j < K; j++) {
+      double cand = tq[j];
+      asm volatile("" : "+v"(cand));
+      q_thr = nsq == j ? cand : q_thr;
+    }
+    left -= (!is_o && !has_q) ? 1 : 0;  // an order completed
+    const bool new_order = !has_q && left > 0;
+    const bool new_region = !has_q && left <= 0 && r + 1 < R;
+    st = has_q ? PS_QTY : new_order ? PS_MASK : new_region ? PS_ORD : PS_DONE;
+    thr = has_q ? q_thr : new_order ? tk : to_next;
+    sq = nsq;
+    mask = new_order ? 0u : mask;
+    if (new_order) {
+      n += 1;
+      recp += rstride;
+      if (n <= cap) {
+#pragma unroll
+        for (int j = 0; j < NV; j++)
+          *reinterpret_cast<MSC_GLOBAL v4u*>(recp + (int64_t)j * E * 16) = v4u{j == 0 ? (unsigned)r : 0u, 0u, 0u, 0u};
+      }
+    }
+    if (new_region) {
+      r += 1;
+      tk = Tk[r];
+      to_next = To[r + 1 < R ? r + 1 : r];
+#pragma unroll
+      for (int j = 0; j < K; j++) tq[j] = Tq[r * K + j];
+    }
+    prod = 1.0;
+    x = 0;
+    mf = st == PS_MASK ? 1 : 0;
+    live = st != PS_DONE ? 1 : 0;
+  };
+  PROF_DECL(p_all);
+  PROF_DECL(n_round);
+  PROF_DECL(n_chunk);
+  PROF_DECL(p_bar);
+  PROF_T(t_start);
+  for (int ci = 0;; ci++) {
+#pragma unroll 1
+    for (int hs = 0; hs < UHS; hs++) {
+      // issue this round's ring reads first, then book the unit that ended last round (its
+      // bookkeeping has no LDS dependence) while they are in flight
+      const double* rp = myring + (rd & (UCAP - 1));
+      double u[UD];
+#pragma unroll
+      for (int i = 0; i < UD; i++) u[i] = rp[i];
+      if (pend) settle();
+      // Poisson unit: p_i = p_{i-1} * U_i in draw order; U_i < 1 makes the products non-increasing,
+      // so "p_i > exp(-lambda)" holds for a leading run only and its length is a plain count.
+      // Mask unit: the K Bernoulli draws, bit i = SKU drawn <=> U_i < p <=> !(U_i > p_skip).
+      double p = prod;
+      int ncont = 0;
+      unsigned bits = 0;
+#pragma unroll
+      for (int i = 0; i < UD; i++) {
+        p = p * u[i];
+        ncont += p > thr ? 1 : 0;
+        if (i < K) bits |= u[i] > thr ? 0u : (1u << i);
+      }
+      const int go = ncont >= UD ? 1 : 0;  // Poisson unit still running after UD draws
+      const int cons = mf ? K : (go ? UD : ncont + 1);
+      mask = mf ? bits : mask;
+      x += ncont;  // (a mask unit's x is unused and cleared by its settle)
+      prod = p;
+      rd += live ? cons : 0;
+      pend = live & (mf | (go ^ 1));
+      PROF_ADD(n_round, 1);
+    }
+    // a lane with a booked-but-unsettled unit is still live: it settles in the next round
+    const bool any = __ballot(live) != 0;
+    rdv[((ci + 1) & 1) * BS + lane] = rd;
+    if (lane == 0) more[ci & 1] = any ? 1 : 0;
+    PROF_T(tb);
+    __syncthreads();
+    PROF_ADD(p_bar, PROF_NOW() - tb);
+    PROF_ADD(n_chunk, 1);
+    if (!any) break;
+  }
+  PROF_ADD(p_all, PROF_NOW() - t_start);
+  PROF_FLUSH(0, p_all);
+  PROF_FLUSH(2, p_bar);
+  PROF_FLUSH(4, n_round);
+  PROF_FLUSH(5, n_chunk);
+  PROF_FLUSH(6, 1ull);
+  if (!valid) return;
+  pcg_advance(r0, (uint64_t)rd);
+  store_rng(s, 0, e, E, r0);
+  if (n > cap) {
+    atomicOr(s.err, ERR_ORDER_OVERFLOW);
+    n = cap;
+  }
+  s.n_orders[e] = n;
+}
+
 // Variant with branchy settling (kept for A/B measurement: MSC_DEMAND_IMPL=flat_branchy).
 //
 // The reference's draw sequence per step is: for each region, Poisson(lambda_o) (multiplication
@@ -2157,12 +2394,29 @@ hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask,
   return hipGetLastError();
 }
 
-static size_t park_fixed(const EnvConst& c) { return c.demand_impl == 4 ? park_lds_fixed() : park4_lds_fixed(); }
+static size_t park_fixed(const EnvConst& c) {
+  return c.demand_impl == 4 ? park_lds_fixed() : c.demand_impl == 5 ? park4_lds_fixed() : unit_lds_fixed();
+}
 static bool park_lds_tables(const EnvConst& c) {
-  return park_fixed(c) + (size_t)(2 + c.K) * c.R * sizeof(double) <= 32 * 1024;
+  return park_fixed(c) + (size_t)(2 + c.K) * c.R * sizeof(double) <= 40 * 1024;
 }
 size_t demand_lds_bytes(const EnvConst& c) {
   return park_fixed(c) + (park_lds_tables(c) ? (size_t)(2 + c.K) * c.R * sizeof(double) : 0);
+}
+
+template <int K, int G>
+static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t st) {
+  using DFn = void (*)(const DevEnv*);
+  const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
+  const bool t = park_lds_tables(c);
+  DFn fn;
+  if (c.demand_impl == 4)  // single-draw hot steps (A/B: MSC_DEMAND_IMPL=park1)
+    fn = t ? (DFn)demand_park_kernel<K, G, true> : (DFn)demand_park_kernel<K, G, false>;
+  else if (c.demand_impl == 5)  // 4-draw parking parser (A/B: MSC_DEMAND_IMPL=park4)
+    fn = t ? (DFn)demand_park4_kernel<K, G, true> : (DFn)demand_park4_kernel<K, G, false>;
+  else
+    fn = t ? (DFn)demand_unit_kernel<K, G, true> : (DFn)demand_unit_kernel<K, G, false>;
+  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), park_fixed(c) + (t ? tab : 0), st, d);
 }
 
 template <int K>
@@ -2177,20 +2431,12 @@ static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st) 
       hipLaunchKernelGGL((demand_flat_kernel<K, true>), grid_for(c.E, c.epw_dem), dim3(BS), lds, st, d);
     else
       hipLaunchKernelGGL((demand_flat_kernel<K, false>), grid_for(c.E, c.epw_dem), dim3(BS), 0, st, d);
+  } else if (c.demand_gen == 1) {
+    launch_split_demand<K, 1>(c, d, st);
+  } else if (c.demand_gen == 3) {
+    launch_split_demand<K, 3>(c, d, st);
   } else {
-    using DFn = void (*)(const DevEnv*);
-    const size_t fixed = park_fixed(c);
-    const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
-    const bool t = park_lds_tables(c);
-    const int G = c.demand_gen == 1 ? 1 : 2;
-    DFn fn;
-    if (c.demand_impl == 4)  // single-draw hot steps (A/B: MSC_DEMAND_IMPL=park1)
-      fn = G == 1 ? (t ? (DFn)demand_park_kernel<K, 1, true> : (DFn)demand_park_kernel<K, 1, false>)
-                  : (t ? (DFn)demand_park_kernel<K, 2, true> : (DFn)demand_park_kernel<K, 2, false>);
-    else
-      fn = G == 1 ? (t ? (DFn)demand_park4_kernel<K, 1, true> : (DFn)demand_park4_kernel<K, 1, false>)
-                  : (t ? (DFn)demand_park4_kernel<K, 2, true> : (DFn)demand_park4_kernel<K, 2, false>);
-    hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), fixed + (t ? tab : 0), st, d);
+    launch_split_demand<K, 2>(c, d, st);
   }
 }
 
