@@ -2082,7 +2082,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   if (dbg && ev && w == 0 && info.n_orders) info.n_orders[e] = n_orders;
   constexpr int NVR = Rec<K>::NV;
   const int64_t rec_step = stride * NVR;
-  const int maxwh = c.max_wh;
+  // per-SKU constants and flags in registers (read once: the loop below stores to global memory,
+  // so the compiler could not keep re-reading them through `c` out of the loop)
+  const int maxwh = c.max_wh, lost_type = c.lost_type, pps = c.pen_per_sku;
+  const double alpha = c.alpha;
+  double skw[K], penk[K];
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) {
+    skw[sk] = c.skw[sk];
+    penk[sk] = pps ? c.pen[sk] : c.pen_scalar;
+  }
+  const MSC_GLOBAL double* ofT = gp(c.ofT);
+  const MSC_GLOBAL double* ovT = gp(c.ovT);
+  const MSC_GLOBAL int32_t* closest = gp(c.closest);
+  const MSC_GLOBAL uint32_t* home_mask = gp(c.home_mask);
+  const int lane = threadIdx.x & 63, gbase = lane & ~(GW - 1);
   int cur = -1, lost_cnt = 0;
   int u[K], dsum[K];
 #pragma unroll
@@ -2094,25 +2108,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     if (lost_cnt > 0) {
       double upen = 0.0;
 #pragma unroll
-      for (int sk = 0; sk < K; sk++)
-        upen += c.pen_per_sku ? (double)u[sk] * c.pen[sk] : ((double)u[sk] * c.skw[sk]) * c.pen_scalar;
+      for (int sk = 0; sk < K; sk++) upen += pps ? (double)u[sk] * penk[sk] : ((double)u[sk] * skw[sk]) * penk[sk];
       double wt = 0.0;  // this warehouse's share of the region's lost sales
-      if (c.lost_type == MSC_LOST_CLOSEST) {
-        wt = (wl && w == c.closest[r]) ? 1.0 : 0.0;
-      } else if (c.lost_type == MSC_LOST_SHIPMENT) {
+      if (lost_type == MSC_LOST_CLOSEST) {
+        wt = (wl && w == closest[r]) ? 1.0 : 0.0;
+      } else if (lost_type == MSC_LOST_SHIPMENT) {
         int acc = 0;
 #pragma unroll
         for (int sk = 0; sk < K; sk++) acc += qsr[sk];
-        const double qr = wl ? (double)acc : 0.0;
-        // integer-valued: exact in any summation order
-        const double tot = group_reduce<GW>(qr, [](double a, double b) { return a + b; });
-        if (tot > 0.0) wt = qr > 0.0 ? qr / tot : 0.0;
-        else wt = (wl && w == c.closest[r]) ? 1.0 : 0.0;
+        acc = wl ? acc : 0;
+        // integer-valued shares: the integer group sum is the f64 sum exactly
+        const int tot = group_reduce<GW>(acc, [](int a, int b) { return a + b; });
+        if (tot > 0) wt = acc > 0 ? (double)acc / (double)tot : 0.0;
+        else wt = (wl && w == closest[r]) ? 1.0 : 0.0;
       } else {  // cost: softmax(-(of * lost_orders + ov * lost_weight) / alpha), numpy sum order
         double lw = 0.0;
 #pragma unroll
-        for (int sk = 0; sk < K; sk++) lw += (double)u[sk] * c.skw[sk];
-        const double lg = wl ? -(cof * (double)lost_cnt + cov * lw) / c.alpha : -INFINITY;
+        for (int sk = 0; sk < K; sk++) lw += (double)u[sk] * skw[sk];
+        const double lg = wl ? -(cof * (double)lost_cnt + cov * lw) / alpha : -INFINITY;
         const double mx = group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
         const double ex = wl ? exp(lg - mx) : 0.0;
         double all[16];
@@ -2129,7 +2142,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
       }
     }
     // home-region features: incoming demand and units shipped home (multi_env.py:767-773)
-    if (wl && (c.home_mask[r] >> w & 1u)) {
+    if (wl && (home_mask[r] >> w & 1u)) {
 #pragma unroll
       for (int sk = 0; sk < K; sk++) {
         s.inc[(int64_t)(w * K + sk) * E + e] = dsum[sk];
@@ -2154,6 +2167,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   for (int q = 0; q < PF; q++)
 #pragma unroll
     for (int j = 0; j < NVR; j++) ring[q][j] = (q < n_orders) ? gload4(src, q * rec_step + j * stride) : make_uint4(0, 0, 0, 0);
+  // outbound cost row of the NEXT order's region, loaded one order ahead (L2-resident table)
+  double pcof = 0.0, pcov = 0.0;
+  if (n_orders > 0 && wl) {
+    const int r0 = (int)(ring[0][0].x & 0xffffu);
+    pcof = ofT[r0 * W + w];
+    pcov = ovT[r0 * W + w];
+  }
+  constexpr int NP = (K + 1) / 2;  // 32-bit words of a packed (16-bit per SKU) fill vector
   for (int oi = 0; oi <= n_orders; oi++) {
     int r = -1;
     int d[K];
@@ -2178,58 +2199,76 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     }
     if (r != cur) {
       if (cur >= 0) finalize(cur);
-      if (r >= 0 && wl) {
-        cof = c.ofT[r * W + w];
-        cov = c.ovT[r * W + w];
-      }
+      cof = pcof;
+      cov = pcov;
       cur = r;
       lost_cnt = 0;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
     }
     if (oi == n_orders) break;
+    if (oi + 1 < n_orders && wl) {
+      const int rn = (int)(ring[0][0].x & 0xffffu);
+      pcof = ofT[rn * W + w];
+      pcov = ovT[rn * W + w];
+    }
     bool any_d = false;
     double tw = 0.0;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       dsum[sk] += d[sk];
       any_d |= d[sk] > 0;
-      tw += (double)d[sk] * c.skw[sk];
+      tw += (double)d[sk] * skw[sk];
     }
     if (!any_d) continue;  // an empty order ships nothing and is never lost
     int rem[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
     const double mycost = cof + cov * tw;  // demand_allocator.py:168-172
-    bool used_me = false;
+    // total-order key of the cost (negatives and -0.0 included), so the group min is an integer min
+    const uint64_t cb = (uint64_t)__double_as_longlong(mycost + 0.0);
+    const uint64_t ckey = cb ^ ((uint64_t)((int64_t)cb >> 63) | 0x8000000000000000ull);
     int used = 0;
     bool open = true;
     while (open) {
+      // a warehouse that shipped already has nothing left that the order still needs
+      // (fill = min(rem, inv) zeroes one of the two for every SKU), so "has" alone excludes it
       bool has = false;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) has |= rem[sk] > 0 && inv[sk] > 0;
-      double bc = (has && wl && !used_me) ? mycost : INFINITY;
-      int bw = w;
-      auto amin = [&](auto step) {  // group argmin, lowest warehouse on ties
-        const double oc = step(bc);
-        const int ow = step(bw);
-        const bool take = oc < bc || (oc == bc && ow < bw);
-        bc = take ? oc : bc;
-        bw = take ? ow : bw;
-      };
-      amin([](auto v) { return dpp_x<0>(v); });
-      if constexpr (GW >= 4) amin([](auto v) { return dpp_x<1>(v); });
-      if constexpr (GW >= 8) amin([](auto v) { return dpp_x<2>(v); });
-      if constexpr (GW >= 16) amin([](auto v) { return dpp_x<3>(v); });
-      if (bc == INFINITY) break;  // nobody holds a still-needed SKU
+      const uint64_t key = (has && wl) ? ckey : ~0ull;
+      uint64_t mk = key;
+      {
+        auto step = [&](uint64_t o) { mk = o < mk ? o : mk; };
+        auto dpp64 = [](auto f, uint64_t v) {
+          const int lo = f((int)(unsigned)v), hi = f((int)(unsigned)(v >> 32));
+          return ((uint64_t)(unsigned)hi << 32) | (unsigned)lo;
+        };
+        step(dpp64([](int v) { return dpp_x<0>(v); }, mk));
+        if constexpr (GW >= 4) step(dpp64([](int v) { return dpp_x<1>(v); }, mk));
+        if constexpr (GW >= 8) step(dpp64([](int v) { return dpp_x<2>(v); }, mk));
+        if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
+      }
+      if (mk == ~0ull) break;  // nobody holds a still-needed SKU
+      // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
+      const uint64_t tie = __ballot(key == mk);
+      const int bw = __builtin_ctzll(tie >> gbase);
       const bool me = w == bw;
       int fl[K];
 #pragma unroll
       for (int sk = 0; sk < K; sk++) fl[sk] = me ? (rem[sk] < inv[sk] ? rem[sk] : inv[sk]) : 0;
+      // the winner's fill reaches every lane: 16-bit fields (fill <= order quantity < 2^16),
+      // one nonzero contributor per group, so an OR reduction is the broadcast
+      unsigned pk[NP];
+#pragma unroll
+      for (int j = 0; j < NP; j++)
+        pk[j] = (unsigned)fl[2 * j] | (2 * j + 1 < K ? (unsigned)fl[2 * j + 1] << 16 : 0u);
+#pragma unroll
+      for (int j = 0; j < NP; j++) pk[j] = (unsigned)group_reduce<GW>((int)pk[j], [](int a, int b) { return a | b; });
       bool done = true;
 #pragma unroll
-      for (int sk = 0; sk < K; sk++) {  // the winner's fill reaches every lane as a group sum
-        rem[sk] -= group_reduce<GW>(fl[sk], [](int a, int b) { return a + b; });
+      for (int sk = 0; sk < K; sk++) {
+        rem[sk] -= (int)((pk[sk >> 1] >> (16 * (sk & 1))) & 0xffffu);
         done &= rem[sk] <= 0;
       }
       if (me) {
@@ -2241,10 +2280,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
           qsr[sk] += fl[sk];
           sht[sk] += fl[sk];
           fsum += fl[sk];
-          fw += (double)fl[sk] * c.skw[sk];
+          fw += (double)fl[sk] * skw[sk];
         }
-        out += fw == tw ? bc : cof + cov * fw;  // whole order from here: the ranking cost bit for bit
-        used_me = true;
+        out += fw == tw ? mycost : cof + cov * fw;  // whole order from here: the ranking cost bit for bit
         if (dbg) {
 #pragma unroll
           for (int sk = 0; sk < K; sk++) {
