@@ -152,12 +152,13 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       ovT[(size_t)r * W + w] = d->outbound_variable[(size_t)w * R + r];
     }
   std::vector<uint32_t> home_mask(R, 0u);
-  std::vector<int32_t> closest(R, 0);
+  std::vector<int32_t> closest(R, 0), home_of(W, 0);
   for (int w = 0; w < W; w++) {  // argmin over regions (first minimum), multi_env.py:144
     int b = 0;
     for (int r = 1; r < R; r++)
       if (d->distances[(size_t)w * R + r] < d->distances[(size_t)w * R + b]) b = r;
     home_mask[b] |= 1u << w;
+    home_of[w] = b;
   }
   for (int r = 0; r < R; r++) {  // argmin over warehouses, lost_sales_handler.py:36
     int b = 0;
@@ -258,6 +259,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
                              sizeof(int32_t) * (d->lead_type == MSC_LEAD_STOCHASTIC && d->max_dev_per_sku ? K : 1));
   const size_t o_hm = tp.add(home_mask.data(), sizeof(uint32_t) * R);
   const size_t o_cl = tp.add(closest.data(), sizeof(int32_t) * R);
+  const size_t o_ho = tp.add(home_of.data(), sizeof(int32_t) * W);
   const size_t o_mean = tp.add(c.norm == MSC_OBS_MEANSTD ? d->obs_mean : zeros_f.data(), sizeof(float) * zeros_f.size());
   const size_t o_std = tp.add(c.norm == MSC_OBS_MEANSTD ? d->obs_std : ones_f.data(), sizeof(float) * ones_f.size());
   size_t o_toff = 0, o_trec = 0;
@@ -298,6 +300,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   c.maxdev = (const int32_t*)(tb + o_md);
   c.home_mask = (const uint32_t*)(tb + o_hm);
   c.closest = (const int32_t*)(tb + o_cl);
+  c.home_of = (const int32_t*)(tb + o_ho);
   c.obs_mean = (const float*)(tb + o_mean);
   c.obs_std = (const float*)(tb + o_std);
   if (d->demand_type == MSC_DEMAND_EMPIRICAL) {

@@ -57,6 +57,7 @@ struct EnvConst {
   const MSC_G int32_t* maxdev;     // [K] or [1]
   const MSC_G uint32_t* home_mask; // [R] bit w set <=> region r is warehouse w's home region
   const MSC_G int32_t* closest;    // [R] closest warehouse of each region
+  const MSC_G int32_t* home_of;    // [W] home region of each warehouse (the bit set in home_mask)
   const MSC_G float* obs_mean;     // [F]
   const MSC_G float* obs_std;      // [F]
   const MSC_G int64_t* tr_off;     // [tr_rows + 1]

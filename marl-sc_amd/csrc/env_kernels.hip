@@ -963,17 +963,20 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_park4_kernel(const DevEnv
 // With no park check, no ballot and no lane-mask logic the round is straight-line code, and a
 // wave runs for ~ max over its lanes of (units + overflow segments) ~ 1.4k rounds at 8x64x5
 // instead of ~3k hot steps + ~1.5k settle passes of demand_park4_kernel.
-// Ring: lane-major [64][USTR], slot = position mod UCAP; slots 0..UD-2 are mirrored at UCAP..
-// so the UD reads of a round are one base address + immediate offsets (no wrap arithmetic).
+// Ring: slot-major [USLOTS][64] (lane fastest), slot = position mod UCAP; slots 0..UD-2 are
+// mirrored at UCAP.. so the UD reads of a round are one base address + immediate offsets (no wrap
+// arithmetic). Every lane reads its own slot, and the lanes' slots differ, so only a layout whose
+// bank depends on the lane alone is conflict-free: [slot][lane] maps lane l to banks 2l, 2l + 1
+// (mod 64) whatever the slot, and the generator's writes of one position are one contiguous row.
 // ------------------------------------------------------------------------------------------
 constexpr int UD = 8;                       // uniforms per round
 constexpr int UHS = 4;                      // rounds per chunk (<= UD * UHS draws per lane)
 constexpr int UCAP = 2 * UD * UHS;          // ring capacity (positions)
-constexpr int USTR = UCAP + UD - 1;         // lane stride in doubles (odd: conflict-free b64 reads)
-static_assert((UCAP & (UCAP - 1)) == 0 && (USTR & 1) == 1, "ring layout");
+constexpr int USLOTS = UCAP + UD - 1;       // ring rows incl. the mirrored ones
+static_assert((UCAP & (UCAP - 1)) == 0, "ring layout");
 
 __host__ __device__ constexpr size_t unit_lds_fixed() {
-  return (size_t)BS * USTR * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
+  return (size_t)BS * USLOTS * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
 }
 
 template <int K, int G, bool LDS_TAB>
@@ -985,13 +988,13 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv*
   constexpr int NW = 4 * NV;
   extern __shared__ __attribute__((aligned(16))) double plds[];
   __shared__ int more[2];
-  double* ring = plds;                                           // [BS][USTR]
-  int32_t* rdv = reinterpret_cast<int32_t*>(plds + BS * USTR);   // [2][BS]
+  double* ring = plds;                                             // [USLOTS][BS]
+  int32_t* rdv = reinterpret_cast<int32_t*>(plds + BS * USLOTS);   // [2][BS]
   const double* To = c.enlam_o;
   const double* Tk = c.p_skip;
   const double* Tq = c.enlam_q;
   if constexpr (LDS_TAB) {
-    double* lo = plds + BS * USTR + BS;
+    double* lo = plds + BS * USLOTS + BS;
     double* lk = lo + R;
     double* lq = lk + R;
     for (int i = threadIdx.x; i < R; i += blockDim.x) {
@@ -1007,7 +1010,7 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv*
   const int64_t E = c.E;
   const int64_t e = (int64_t)blockIdx.x * c.epw_dem + lane;
   const bool valid = lane < c.epw_dem && e < E;
-  double* myring = ring + lane * USTR;
+  double* myring = ring + lane;
 
   if (wave > 0) {
     // ---------------- generator g: stream positions g, g + G, g + 2G, ...
@@ -1028,8 +1031,8 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv*
       while (pg < target) {
         const double u = u64_to_double(pcg_output(th, tl));
         const int slot = pg & (UCAP - 1);
-        myring[slot] = u;
-        if (slot < UD - 1) myring[slot + UCAP] = u;
+        myring[slot * BS] = u;
+        if (slot < UD - 1) myring[(slot + UCAP) * BS] = u;
         uint64_t nh, nl;
         mul128(th, tl, mh, ml, nh, nl);
         add128(nh, nl, ch, cl);
@@ -1135,10 +1138,10 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv*
     for (int hs = 0; hs < UHS; hs++) {
       // issue this round's ring reads first, then book the unit that ended last round (its
       // bookkeeping has no LDS dependence) while they are in flight
-      const double* rp = myring + (rd & (UCAP - 1));
+      const double* rp = myring + (rd & (UCAP - 1)) * BS;
       double u[UD];
 #pragma unroll
-      for (int i = 0; i < UD; i++) u[i] = rp[i];
+      for (int i = 0; i < UD; i++) u[i] = rp[i * BS];
       if (pend) settle();
       // Poisson unit: p_i = p_{i-1} * U_i in draw order; U_i < 1 makes the products non-increasing,
       // so "p_i > exp(-lambda)" holds for a leading run only and its length is a plain count.
@@ -2044,7 +2047,29 @@ __device__ __forceinline__ T group_reduce(T v, F op) {
   return v;
 }
 
-template <int K, int GW, bool DBG>
+// Order records reach the allocator through a wave-private, double-buffered LDS window filled by
+// LDS-DMA (global_load_lds_dwordx4: no VGPR staging): while the wave allocates the SB_CH orders
+// of one window, the next window is in flight, so the order loop has no global-memory wait (a
+// register FIFO of prefetched records waited on its newest load at every shift).
+constexpr int SB_REC = 128;  // records per window (2 KiB), two windows per wave
+__host__ __device__ constexpr int step_b_chunk(int GW, int NV) { return SB_REC / ((64 / GW) * NV); }
+// block tables: outbound costs [2][R][W] f64 + closest warehouse [R], staged in LDS when small
+__host__ __device__ constexpr size_t step_b_tab_bytes(int R, int W) {
+  return (size_t)2 * R * W * sizeof(double) + (size_t)R * sizeof(int32_t);
+}
+constexpr size_t STEP_B_TAB_MAX = 16 * 1024;
+__host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab) {
+  return (size_t)4 * 2 * SB_REC * 16 + (tab ? step_b_tab_bytes(R, W) : 0);
+}
+
+// a wave-uniform double kept in scalar registers
+__device__ __forceinline__ double sgpr_d(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <int K, int GW, bool DBG, bool TAB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
@@ -2055,49 +2080,109 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   const bool ev = e < E, wl = w < W;
   const msc_step_info info = io.info;
   constexpr bool dbg = DBG;
-  int inv[K], qsr[K], sht[K], shh[K];
+  constexpr int NVR = Rec<K>::NV;
+  constexpr int EPW = 64 / GW;                // envs per wave
+  constexpr int CH = SB_REC / (EPW * NVR);    // orders per window
+  constexpr int LPL = SB_REC / 64;            // LDS-DMA loads per lane per window
+  static_assert(CH >= 1 && SB_REC % 64 == 0, "window layout");
+  extern __shared__ __attribute__((aligned(16))) uint4 sb_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, gbase = lane & ~(GW - 1);
+  uint4* win = sb_lds + wave * 2 * SB_REC;  // this wave's two windows [2][CH][NVR][EPW]
+  const MSC_GLOBAL int32_t* closest = gp(c.closest);
+  double* lof = TAB ? reinterpret_cast<double*>(sb_lds + 4 * 2 * SB_REC) : nullptr;
+  double* lov = TAB ? lof + R * W : nullptr;
+  int32_t* lcl = TAB ? reinterpret_cast<int32_t*>(lov + R * W) : nullptr;
+  if constexpr (TAB) {
+    for (int i = threadIdx.x; i < R * W; i += blockDim.x) {
+      lof[i] = c.ofT[i];
+      lov[i] = c.ovT[i];
+    }
+    for (int i = threadIdx.x; i < R; i += blockDim.x) lcl[i] = c.closest[i];
+    __syncthreads();
+  }
+  auto cost_of = [&](int r) { return TAB ? lof[r * W + w] : gp(c.ofT)[r * W + w]; };
+  auto cost_ov = [&](int r) { return TAB ? lov[r * W + w] : gp(c.ovT)[r * W + w]; };
+  auto closest_of = [&](int r) { return TAB ? lcl[r] : closest[r]; };
+
+  int inv[K], qsr[K];
 #pragma unroll
   for (int sk = 0; sk < K; sk++) {
     inv[sk] = (ev && wl) ? s.inv[(int64_t)(w * K + sk) * E + e] : 0;
-    qsr[sk] = sht[sk] = shh[sk] = 0;
+    qsr[sk] = 0;
   }
   double pen = 0.0, out = 0.0, cof = 0.0, cov = 0.0;
   int n_orders = 0;
-  const MSC_GLOBAL uint4* src;
-  int64_t stride;
+  // record (n, v) of this lane's env at base + n * nstep + v * vstep (uint4 units)
+  int64_t base = 0, nstep, vstep;
   if (c.demand_type == MSC_DEMAND_EMPIRICAL) {
-    int64_t off = 0;
     if (ev) {
       const int64_t row = s.emp_start[e] + (s.t[e] % c.T);
-      off = c.tr_off[row];
+      const int64_t off = c.tr_off[row];
       n_orders = (int)(c.tr_off[row + 1] - off);
+      base = off * NVR;
     }
-    src = gp(c.tr_rec + off * Rec<K>::NV);
-    stride = 1;
+    nstep = NVR;
+    vstep = 1;
   } else {
     n_orders = ev ? s.n_orders[e] : 0;
-    src = gp(s.orders + (ev ? e : 0));
-    stride = E;
+    base = ev ? e : 0;
+    nstep = (int64_t)NVR * E;
+    vstep = E;
   }
+  const MSC_GLOBAL uint4* src = gp(c.demand_type == MSC_DEMAND_EMPIRICAL ? c.tr_rec : s.orders);
   if (dbg && ev && w == 0 && info.n_orders) info.n_orders[e] = n_orders;
-  constexpr int NVR = Rec<K>::NV;
-  const int64_t rec_step = stride * NVR;
+  // loader role: lane l fetches records of env l % EPW of this wave (whose group leader is lane
+  // (l % EPW) * GW); window slot q = j * 64 + l holds (order q / (EPW NVR), v, env q % EPW)
+  const int ljj = lane % EPW;
+  const int ln = __shfl(n_orders, ljj * GW);
+  const int64_t lbase = __shfl(base, ljj * GW);
+  int wmax = n_orders;  // orders of the wave's busiest env
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int v = __shfl_xor(wmax, o);
+    wmax = v > wmax ? v : wmax;
+  }
+  auto issue = [&](int chunk) {  // LDS-DMA of window `chunk` into buffer chunk % 2
+    uint4* dst = win + (chunk & 1) * SB_REC;
+#pragma unroll
+    for (int j = 0; j < LPL; j++) {
+      const int ov = (j * 64 + lane) / EPW;
+      const int n = chunk * CH + ov / NVR, v = ov % NVR;
+      // (inline asm: with the builtin the compiler drains every LDS-DMA in flight before any LDS
+      // read, i.e. at each order; the explicit counted waits below order the windows instead)
+      const uint32_t lds = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(dst + j * 64));
+      const MSC_GLOBAL uint4* g = src + lbase + n * nstep + v * vstep;
+      if (n < ln) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(g), "s"(lds)
+                     : "memory");
+      }
+    }
+  };
+  issue(0);
+  if (wmax > CH) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPL) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   // per-SKU constants and flags in registers (read once: the loop below stores to global memory,
   // so the compiler could not keep re-reading them through `c` out of the loop)
   const int maxwh = c.max_wh, lost_type = c.lost_type, pps = c.pen_per_sku;
-  const double alpha = c.alpha;
-  double skw[K], penk[K];
+  const double alpha = sgpr_d(c.alpha);
+  double skw[K], penk[K];  // wave-uniform: moved to SGPRs (the loads themselves are vector loads)
 #pragma unroll
   for (int sk = 0; sk < K; sk++) {
-    skw[sk] = c.skw[sk];
-    penk[sk] = pps ? c.pen[sk] : c.pen_scalar;
+    skw[sk] = sgpr_d(c.skw[sk]);
+    penk[sk] = sgpr_d(pps ? c.pen[sk] : c.pen_scalar);
   }
-  const MSC_GLOBAL double* ofT = gp(c.ofT);
-  const MSC_GLOBAL double* ovT = gp(c.ovT);
-  const MSC_GLOBAL int32_t* closest = gp(c.closest);
-  const MSC_GLOBAL uint32_t* home_mask = gp(c.home_mask);
-  const int lane = threadIdx.x & 63, gbase = lane & ~(GW - 1);
+  // this warehouse's home region (argmin over regions of its distance row, multi_env.py:144)
+  const int myhome = wl ? c.home_of[w] : -1;
   int cur = -1, lost_cnt = 0;
+  bool home_done = false;
   int u[K], dsum[K];
 #pragma unroll
   for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
@@ -2111,7 +2196,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
       for (int sk = 0; sk < K; sk++) upen += pps ? (double)u[sk] * penk[sk] : ((double)u[sk] * skw[sk]) * penk[sk];
       double wt = 0.0;  // this warehouse's share of the region's lost sales
       if (lost_type == MSC_LOST_CLOSEST) {
-        wt = (wl && w == closest[r]) ? 1.0 : 0.0;
+        wt = (wl && w == closest_of(r)) ? 1.0 : 0.0;
       } else if (lost_type == MSC_LOST_SHIPMENT) {
         int acc = 0;
 #pragma unroll
@@ -2120,7 +2205,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
         // integer-valued shares: the integer group sum is the f64 sum exactly
         const int tot = group_reduce<GW>(acc, [](int a, int b) { return a + b; });
         if (tot > 0) wt = acc > 0 ? (double)acc / (double)tot : 0.0;
-        else wt = (wl && w == closest[r]) ? 1.0 : 0.0;
+        else wt = (wl && w == closest_of(r)) ? 1.0 : 0.0;
       } else {  // cost: softmax(-(of * lost_orders + ov * lost_weight) / alpha), numpy sum order
         double lw = 0.0;
 #pragma unroll
@@ -2142,12 +2227,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
       }
     }
     // home-region features: incoming demand and units shipped home (multi_env.py:767-773)
-    if (wl && (home_mask[r] >> w & 1u)) {
+    if (r == myhome) {
 #pragma unroll
       for (int sk = 0; sk < K; sk++) {
         s.inc[(int64_t)(w * K + sk) * E + e] = dsum[sk];
-        shh[sk] = qsr[sk];
+        s.sc_shh[(int64_t)(w * K + sk) * E + e] = qsr[sk];
       }
+      home_done = true;
     }
     if (dbg && w == 0) {
 #pragma unroll
@@ -2161,21 +2247,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     for (int sk = 0; sk < K; sk++) qsr[sk] = 0;
   };
 
-  constexpr int PF = 4;
-  uint4 ring[PF][NVR];
-#pragma unroll
-  for (int q = 0; q < PF; q++)
-#pragma unroll
-    for (int j = 0; j < NVR; j++) ring[q][j] = (q < n_orders) ? gload4(src, q * rec_step + j * stride) : make_uint4(0, 0, 0, 0);
-  // outbound cost row of the NEXT order's region, loaded one order ahead (L2-resident table)
-  double pcof = 0.0, pcov = 0.0;
-  if (n_orders > 0 && wl) {
-    const int r0 = (int)(ring[0][0].x & 0xffffu);
-    pcof = ofT[r0 * W + w];
-    pcov = ovT[r0 * W + w];
-  }
   constexpr int NP = (K + 1) / 2;  // 32-bit words of a packed (16-bit per SKU) fill vector
-  for (int oi = 0; oi <= n_orders; oi++) {
+  const int myjj = lane / GW;      // this group's env slot in the window
+  for (int oi = 0; oi <= wmax; oi++) {
+    if (oi > 0 && oi % CH == 0) {  // wave-uniform: window oi / CH is due, start the one after
+      if (oi + CH <= wmax) {
+        issue(oi / CH + 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPL) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    if (oi > n_orders) continue;  // this env is done (lanes of busier envs go on)
     int r = -1;
     int d[K];
     {
@@ -2184,34 +2267,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
         uint16_t h[8 * NVR];
       } ur;
 #pragma unroll
-      for (int j = 0; j < NVR; j++) ur.v[j] = ring[0][j];
+      for (int j = 0; j < NVR; j++) ur.v[j] = win[((oi / CH) & 1) * SB_REC + ((oi % CH) * NVR + j) * EPW + myjj];
       if (oi < n_orders) r = ur.h[0];
 #pragma unroll
       for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
     }
-#pragma unroll
-    for (int q = 0; q + 1 < PF; q++)
-#pragma unroll
-      for (int j = 0; j < NVR; j++) ring[q][j] = ring[q + 1][j];
-    if (oi + PF < n_orders) {
-#pragma unroll
-      for (int j = 0; j < NVR; j++) ring[PF - 1][j] = gload4(src, (oi + PF) * rec_step + j * stride);
-    }
     if (r != cur) {
       if (cur >= 0) finalize(cur);
-      cof = pcof;
-      cov = pcov;
+      if (r >= 0 && wl) {
+        cof = cost_of(r);
+        cov = cost_ov(r);
+      }
       cur = r;
       lost_cnt = 0;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
     }
-    if (oi == n_orders) break;
-    if (oi + 1 < n_orders && wl) {
-      const int rn = (int)(ring[0][0].x & 0xffffu);
-      pcof = ofT[rn * W + w];
-      pcov = ovT[rn * W + w];
-    }
+    if (oi == n_orders) continue;
     bool any_d = false;
     double tw = 0.0;
 #pragma unroll
@@ -2226,8 +2298,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
     const double mycost = cof + cov * tw;  // demand_allocator.py:168-172
     // total-order key of the cost (negatives and -0.0 included), so the group min is an integer min
-    const uint64_t cb = (uint64_t)__double_as_longlong(mycost + 0.0);
-    const uint64_t ckey = cb ^ ((uint64_t)((int64_t)cb >> 63) | 0x8000000000000000ull);
+    const uint64_t cbits = (uint64_t)__double_as_longlong(mycost + 0.0);
+    const uint64_t ckey = cbits ^ ((uint64_t)((int64_t)cbits >> 63) | 0x8000000000000000ull);
     int used = 0;
     bool open = true;
     while (open) {
@@ -2278,7 +2350,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
         for (int sk = 0; sk < K; sk++) {
           inv[sk] -= fl[sk];
           qsr[sk] += fl[sk];
-          sht[sk] += fl[sk];
           fsum += fl[sk];
           fw += (double)fl[sk] * skw[sk];
         }
@@ -2308,9 +2379,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       const int64_t i = (int64_t)(w * K + sk) * E + e;
+      s.sc_sht[i] = s.inv[i] - inv[sk];  // shipped this step = the inventory drop (only shipments lower it here)
       s.inv[i] = inv[sk];
-      s.sc_sht[i] = sht[sk];
-      s.sc_shh[i] = shh[sk];
+      if (!home_done) s.sc_shh[i] = 0;
     }
     s.sc_pen[w * E + e] = pen;
     s.sc_out[w * E + e] = out;
@@ -2493,16 +2564,16 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     const bool dbg = io.has_info != 0;  // collect_step_info: the instrumented instantiations
     KFn a = dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>;
     KFn cc = dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>;
+    const bool tab = step_b_tab_bytes(c.R, c.W) <= STEP_B_TAB_MAX;
     KFn b;
-    if (dbg)
-      b = GW == 2 ? (KFn)step_b_kernel<K, 2, true> : GW == 4 ? (KFn)step_b_kernel<K, 4, true>
-        : GW == 8 ? (KFn)step_b_kernel<K, 8, true> : (KFn)step_b_kernel<K, 16, true>;
-    else
-      b = GW == 2 ? (KFn)step_b_kernel<K, 2, false> : GW == 4 ? (KFn)step_b_kernel<K, 4, false>
-        : GW == 8 ? (KFn)step_b_kernel<K, 8, false> : (KFn)step_b_kernel<K, 16, false>;
+#define MSC_SB(GWV)                                                                                   \
+  (dbg ? (tab ? (KFn)step_b_kernel<K, GWV, true, true> : (KFn)step_b_kernel<K, GWV, true, false>)   \
+       : (tab ? (KFn)step_b_kernel<K, GWV, false, true> : (KFn)step_b_kernel<K, GWV, false, false>))
+    b = GW == 2 ? MSC_SB(2) : GW == 4 ? MSC_SB(4) : GW == 8 ? MSC_SB(8) : MSC_SB(16);
+#undef MSC_SB
     const size_t lds_a = c.lead_type == MSC_LEAD_STOCHASTIC ? (size_t)c.W * K * BS * sizeof(int32_t) : 0;
     hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * c.W), lds_a, st, d, io);
-    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), 0, st, d, io);
+    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
     hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), (size_t)c.W * BS * sizeof(double), st, d, io);
     return hipGetLastError();
   }
