@@ -30,6 +30,10 @@ sys.path.insert(0, str(REPO / "oracle"))
 
 BASELINE = json.loads((REPO / "BASELINE.json").read_text())
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+# VALU issue peak: 256 CUs x 4 SIMD-32 x one wave64 instruction per 2 cycles at 2.4 GHz
+VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
+DEMAND_KERNEL = "demand_unit_kernel"
+STEP_KERNELS = ("step_a_kernel", "step_b_kernel", "step_c_kernel")
 
 
 def ensure_built():
@@ -196,15 +200,25 @@ def main():
         value = E * world * spec.W * K / dt
         mean_orders = float(spec.lambda_orders.sum())
         b_dem, b_step = algorithmic_bytes(spec, mean_orders)
-        kern = {"demand_park_kernel": (t_demand, b_dem * E), "step_kernel": (t_step, b_step * E)}
+        kern = {DEMAND_KERNEL: (t_demand, b_dem * E), "step_kernels": (t_step, b_step * E)}
         dom = max(kern, key=lambda k: kern[k][0])
         t_dom, bytes_dom = kern[dom]
-        traffic = None
+        # per-launch HBM bytes / instruction counts of the same workload from the rocprofv3 PMC
+        # passes (scripts/gpu_profile.sh -> profiles/traffic.json)
+        traffic = valu = None
         tj = Path(args.traffic_json)
+        key = f"{spec.W}x{spec.R}x{spec.K}x{E}"
         if tj.exists():
             tr = json.loads(tj.read_text())
-            key = f"{spec.W}x{spec.R}x{spec.K}x{E}"
-            traffic = tr.get(key, {}).get(dom)
+            names = STEP_KERNELS if dom == "step_kernels" else (dom,)
+            tb = [tr.get(key, {}).get(n) for n in names]
+            traffic = sum(tb) if all(x is not None for x in tb) else None
+            cn = [tr.get("counters", {}).get(key, {}).get(n, {}).get("SQ_INSTS_VALU") for n in names]
+            if all(x is not None for x in cn):
+                ach = sum(cn) / t_dom
+                valu = {"insts_per_launch": int(sum(cn)), "achieved": round(ach / 1e9, 2),
+                        "peak": round(VALU_PEAK_WINST / 1e9, 1), "unit": "G wave-instructions/s",
+                        "frac": round(ach / VALU_PEAK_WINST, 4)}
         achieved = bytes_dom / t_dom / 1e9
         out = {
             "metric": BASELINE["metric"],
@@ -224,11 +238,14 @@ def main():
                        "n_envs_per_gpu": E, "agents": spec.W, "regions": spec.R, "skus": spec.K,
                        "episode_length": spec.episode_length, "obs_dim_local": spec.local_obs_dim,
                        "parallelism": f"env-shard x{world}"},
-            "kernels_ms": {"demand_park_kernel": round(t_demand * 1e3, 4), "step_kernel": round(t_step * 1e3, 4)},
+            "kernels_ms": {DEMAND_KERNEL: round(t_demand * 1e3, 4), "step_kernels": round(t_step * 1e3, 4)},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "bytes_per_launch": int(bytes_dom)},
+                         "traffic": traffic, "bytes_per_launch": int(bytes_dom),
+                         "note": "issue-bound (per-env serial RNG/parse chain), not HBM-bound: see valu_issue and DESIGN.md"},
         }
+        if valu is not None:
+            out["roofline"]["valu_issue"] = valu
         if args.rollout_T > 0:
             out["rollout"] = {
                 "value": round(E * world * spec.W * args.rollout_T / t_roll, 1), "unit": "agent-steps/s",

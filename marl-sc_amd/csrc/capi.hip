@@ -224,7 +224,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
                     : strcmp(impl, "park4") == 0        ? 5
                                                         : 0;
     const char* gen = getenv("MSC_DEMAND_GEN");
-    c.demand_gen = gen && atoi(gen) >= 1 && atoi(gen) <= 3 ? atoi(gen) : 3;
+    c.demand_gen = gen && atoi(gen) >= 1 && atoi(gen) <= 4 ? atoi(gen) : 3;
     auto epw = [](const char* name, int dflt) {
       const char* v = getenv(name);
       const int x = v ? atoi(v) : dflt;
@@ -233,6 +233,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     c.epw_dem = epw("MSC_DEMAND_EPW", 64);
     const char* pm = getenv("MSC_PARK_MIN");
     c.park_min = pm && atoi(pm) >= 1 && atoi(pm) <= 64 ? atoi(pm) : 32;
+    const char* prot = getenv("MSC_PARSER_ROT");
+    c.parser_rot = prot ? atoi(prot) : 0;
     c.epw_step = epw("MSC_STEP_EPW", 64);
     const char* si = getenv("MSC_STEP_IMPL");
     c.step_impl = si && strcmp(si, "lane") == 0 ? 1 : 0;

@@ -34,6 +34,7 @@ struct EnvConst {
   int32_t demand_impl;  // 0 = generator waves + unit-per-round parser (default); A/B: 1 nested, 2 flat_branchy, 3 flat, 4 park1, 5 park4
   int32_t demand_gen;   // generator waves per block of the split demand kernel (1, 2 or 3)
   int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
+  int32_t parser_rot;   // which wave of a demand block parses: (wave + rot(block)) % (1 + G) == 0 (A/B knob)
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
   int32_t epw_step;     // envs per 64-lane block of the lane-per-env step kernel (A/B only)
   int32_t step_impl;    // 0 = group-per-env step kernel (default), 1 = lane-per-env (MSC_STEP_IMPL=lane)

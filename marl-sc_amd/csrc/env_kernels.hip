@@ -972,7 +972,7 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_park4_kernel(const DevEnv
 constexpr int UD = 8;                       // uniforms per round
 constexpr int UHS = 4;                      // rounds per chunk (<= UD * UHS draws per lane)
 constexpr int UCAP = 2 * UD * UHS;          // ring capacity (positions)
-constexpr int USLOTS = UCAP + UD - 1;       // ring rows incl. the mirrored ones
+constexpr int USLOTS = UCAP + UD;           // ring rows: UCAP + the UD - 1 mirrored ones + a dummy row
 static_assert((UCAP & (UCAP - 1)) == 0, "ring layout");
 
 __host__ __device__ constexpr size_t unit_lds_fixed() {
@@ -1006,7 +1006,9 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv*
     Tk = lk;
     Tq = lq;
   }
-  const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;
+  const int rot = c.parser_rot == 1 ? (int)(blockIdx.x >> 8) : c.parser_rot == 2 ? (int)blockIdx.x
+                : c.parser_rot == 3 ? (int)(blockIdx.x >> 3) : 0;
+  const int wave = ((int)(threadIdx.x / BS) + rot) % (1 + G), lane = threadIdx.x % BS;  // role 0 parses
   const int64_t E = c.E;
   const int64_t e = (int64_t)blockIdx.x * c.epw_dem + lane;
   const bool valid = lane < c.epw_dem && e < E;
@@ -1032,7 +1034,7 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv*
         const double u = u64_to_double(pcg_output(th, tl));
         const int slot = pg & (UCAP - 1);
         myring[slot * BS] = u;
-        if (slot < UD - 1) myring[(slot + UCAP) * BS] = u;
+        myring[(slot < UD - 1 ? slot + UCAP : USLOTS - 1) * BS] = u;  // mirror (or the dummy row)
         uint64_t nh, nl;
         mul128(th, tl, mh, ml, nh, nl);
         add128(nh, nl, ch, cl);
@@ -2544,6 +2546,8 @@ static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st) 
     launch_split_demand<K, 1>(c, d, st);
   } else if (c.demand_gen == 3) {
     launch_split_demand<K, 3>(c, d, st);
+  } else if (c.demand_gen == 4) {
+    launch_split_demand<K, 4>(c, d, st);
   } else {
     launch_split_demand<K, 2>(c, d, st);
   }

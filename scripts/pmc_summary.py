@@ -22,6 +22,7 @@ for path in glob.glob(f"gpurun_out/pmc_*_{tag}/**/*counter_collection.csv", recu
         for c, x in v.items():
             out[k][c] = sum(x) / len(x)
 traffic = {}
+counters = {}
 for k, v in sorted(out.items()):
     if "msc::" not in k:
         continue
@@ -32,4 +33,6 @@ for k, v in sorted(out.items()):
     if m and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
         traffic[m.group(1)] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
         print(f"   => HBM traffic per launch {traffic[m.group(1)] / 1e6:.2f} MB (2 x FETCH + WRITE)")
-json.dump({workload: traffic}, open(f"gpurun_out/traffic_{tag}.json", "w"), indent=1)
+    if m:
+        counters[m.group(1)] = {c: v[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES") if c in v}
+json.dump({workload: traffic, "counters": {workload: counters}}, open(f"gpurun_out/traffic_{tag}.json", "w"), indent=1)
