@@ -224,7 +224,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
                     : strcmp(impl, "park4") == 0        ? 5
                                                         : 0;
     const char* gen = getenv("MSC_DEMAND_GEN");
-    c.demand_gen = gen && atoi(gen) >= 1 && atoi(gen) <= 4 ? atoi(gen) : 3;
+    c.demand_gen = gen && ((atoi(gen) >= 1 && atoi(gen) <= 4) || atoi(gen) == 7) ? atoi(gen) : 3;
     auto epw = [](const char* name, int dflt) {
       const char* v = getenv(name);
       const int x = v ? atoi(v) : dflt;

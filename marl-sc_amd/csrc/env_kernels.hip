@@ -969,9 +969,16 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_park4_kernel(const DevEnv
 // bank depends on the lane alone is conflict-free: [slot][lane] maps lane l to banks 2l, 2l + 1
 // (mod 64) whatever the slot, and the generator's writes of one position are one contiguous row.
 // ------------------------------------------------------------------------------------------
-constexpr int UD = 8;                       // uniforms per round
-constexpr int UHS = 4;                      // rounds per chunk (<= UD * UHS draws per lane)
-constexpr int UCAP = 2 * UD * UHS;          // ring capacity (positions)
+#ifndef MSC_UD
+#define MSC_UD 8
+#endif
+#ifndef MSC_UHS
+#define MSC_UHS 4
+#endif
+constexpr int UD = MSC_UD;                  // uniforms per round
+constexpr int UHS = MSC_UHS;                // rounds per chunk (<= UD * UHS draws per lane)
+constexpr int pow2ceil(int x) { return x <= 1 ? 1 : 2 * pow2ceil((x + 1) / 2); }
+constexpr int UCAP = pow2ceil(2 * UD * UHS);  // ring capacity (positions), >= 2 chunks
 constexpr int USLOTS = UCAP + UD;           // ring rows: UCAP + the UD - 1 mirrored ones + a dummy row
 static_assert((UCAP & (UCAP - 1)) == 0, "ring layout");
 
@@ -979,8 +986,12 @@ __host__ __device__ constexpr size_t unit_lds_fixed() {
   return (size_t)BS * USLOTS * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
 }
 
+#ifndef MSC_DEM_WPE
+#define MSC_DEM_WPE 8  // <= 64 VGPRs: two demand waves fit beside four step_b waves on a SIMD
+#endif
 template <int K, int G, bool LDS_TAB>
-__global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv* __restrict__ dp) {
+__global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MSC_DEM_WPE))) void demand_unit_kernel(
+    const DevEnv* __restrict__ dp) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int R = c.R;
@@ -1075,56 +1086,43 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_unit_kernel(const DevEnv*
   const int64_t rstride = (int64_t)NV * E * 16;  // bytes between consecutive records of a lane
   MSC_GLOBAL char* recp = reinterpret_cast<MSC_GLOBAL char*>(gp(s.orders + e)) - rstride;
   __syncthreads();
-  // thresholds of the current region in registers (reloaded when a region starts, long before
-  // their first use): exp(-lambda_q[r, :]), p_skip[r], and exp(-lambda_o[r + 1])
-  double tq[K], tk = Tk[0], to_next = To[R > 1 ? 1 : 0];
-#pragma unroll
-  for (int j = 0; j < K; j++) tq[j] = Tq[j];
+  // p_skip[r] and exp(-lambda_o[r + 1]) of the current region in registers (reloaded when a
+  // region starts, long before their first use); exp(-lambda_q[r, sku]) is read from the LDS
+  // table when a quantity unit opens, while the round's ring reads are in flight
+  double tk = Tk[0], to_next = To[R > 1 ? 1 : 0];
   double prod = 1.0, thr = To[0];
-  // a unit ended: book its result, open the next unit (all lanes with a pending unit, predicated)
+  // a unit ended: book its result, open the next unit (straight-line, predicated; only the two
+  // record stores are guarded)
   auto settle = [&]() {
-    const bool is_q = st == PS_QTY, is_o = st == PS_ORD;
-    if (is_q && n <= cap) {
+    const int is_q = st == PS_QTY ? 1 : 0, is_o = st == PS_ORD ? 1 : 0;
+    if (is_q & (n <= cap ? 1 : 0)) {
       const int h = 1 + sq;  // 16-bit field of the record (field 0 = region)
       *reinterpret_cast<MSC_GLOBAL uint16_t*>(recp + (int64_t)(h >> 3) * E * 16 + (h & 7) * 2) =
           (uint16_t)(x > 1 ? x : 1);  // max(1, Poisson(lambda_q))
     }
-    mask = is_q ? (mask & (mask - 1u)) : mask;
-    left = is_o ? x : left;
-    const bool has_q = !is_o && mask != 0;
-    const int nsq = __builtin_ctz(mask | (1u << K));
-    // register select (the opaque copies keep the compiler from turning the chain back into an
-    // indexed load from a private array, i.e. scratch memory)
-    double q_thr = tq[0];
-#pragma unroll
-    for (int j = 1; j < K; j++) {
-      double cand = tq[j];
-      asm volatile("" : "+v"(cand));
-      q_thr = nsq == j ? cand : q_thr;
-    }
-    left -= (!is_o && !has_q) ? 1 : 0;  // an order completed
-    const bool new_order = !has_q && left > 0;
-    const bool new_region = !has_q && left <= 0 && r + 1 < R;
+    const unsigned m2 = is_q ? (mask & (mask - 1u)) : mask;
+    const int has_q = (is_o ^ 1) & (m2 != 0u ? 1 : 0);
+    const int left2 = (is_o ? x : left) - ((is_o | has_q) ^ 1);  // an order completed
+    const int new_order = (has_q ^ 1) & (left2 > 0 ? 1 : 0);
+    const int new_region = (has_q | new_order) ^ 1 ? (r + 1 < R ? 1 : 0) : 0;
+    int nsq = __builtin_ctz(m2 | (1u << K));
+    nsq = nsq < K ? nsq : K - 1;
+    const double q_thr = Tq[r * K + nsq];
     st = has_q ? PS_QTY : new_order ? PS_MASK : new_region ? PS_ORD : PS_DONE;
     thr = has_q ? q_thr : new_order ? tk : to_next;
     sq = nsq;
-    mask = new_order ? 0u : mask;
-    if (new_order) {
-      n += 1;
-      recp += rstride;
-      if (n <= cap) {
+    mask = new_order ? 0u : m2;
+    left = left2;
+    n += new_order;
+    recp += new_order ? rstride : 0;
+    if (new_order & (n <= cap ? 1 : 0)) {
 #pragma unroll
-        for (int j = 0; j < NV; j++)
-          *reinterpret_cast<MSC_GLOBAL v4u*>(recp + (int64_t)j * E * 16) = v4u{j == 0 ? (unsigned)r : 0u, 0u, 0u, 0u};
-      }
+      for (int j = 0; j < NV; j++)
+        *reinterpret_cast<MSC_GLOBAL v4u*>(recp + (int64_t)j * E * 16) = v4u{j == 0 ? (unsigned)r : 0u, 0u, 0u, 0u};
     }
-    if (new_region) {
-      r += 1;
-      tk = Tk[r];
-      to_next = To[r + 1 < R ? r + 1 : r];
-#pragma unroll
-      for (int j = 0; j < K; j++) tq[j] = Tq[r * K + j];
-    }
+    r += new_region;
+    tk = Tk[r];
+    to_next = To[r + 1 < R ? r + 1 : r];
     prod = 1.0;
     x = 0;
     mf = st == PS_MASK ? 1 : 0;
@@ -2053,7 +2051,10 @@ __device__ __forceinline__ T group_reduce(T v, F op) {
 // LDS-DMA (global_load_lds_dwordx4: no VGPR staging): while the wave allocates the SB_CH orders
 // of one window, the next window is in flight, so the order loop has no global-memory wait (a
 // register FIFO of prefetched records waited on its newest load at every shift).
-constexpr int SB_REC = 128;  // records per window (2 KiB), two windows per wave
+#ifndef MSC_SB_REC
+#define MSC_SB_REC 128
+#endif
+constexpr int SB_REC = MSC_SB_REC;  // records per window (16 B each), two windows per wave
 __host__ __device__ constexpr int step_b_chunk(int GW, int NV) { return SB_REC / ((64 / GW) * NV); }
 // block tables: outbound costs [2][R][W] f64 + closest warehouse [R], staged in LDS when small
 __host__ __device__ constexpr size_t step_b_tab_bytes(int R, int W) {
@@ -2064,6 +2065,45 @@ __host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab) {
   return (size_t)4 * 2 * SB_REC * 16 + (tab ? step_b_tab_bytes(R, W) : 0);
 }
 
+// numpy add.reduce order (np_sum_f64_16) of the group's lane values v_0..v_{n-1} without
+// materialising them: sequential below 8 (lane shuffles), else the 8-accumulator tree as 3 DPP
+// butterfly steps over lanes 0..7 (IEEE addition is commutative, so the butterfly's pairs are
+// numpy's pairs) plus the sequential tail; the result reaches every lane of the group
+template <int GW>
+__device__ __forceinline__ double group_np_sum(double v, int n) {
+  if (n < 8) {
+    double r = 0.0;
+#pragma unroll
+    for (int j = 0; j < (GW < 8 ? GW : 8); j++) {
+      const double x = __shfl(v, j, GW);
+      r = j < n ? r + x : r;
+    }
+    return r;
+  }
+  if constexpr (GW < 8) {
+    return 0.0;  // unreachable: n <= W <= GW
+  } else {
+    const double hi = __shfl(v, (threadIdx.x + 8) % GW, GW);  // v_{k+8} for lane k < 8
+    double a = n >= 16 ? v + hi : v;
+    a = a + dpp_x<0>(a);
+    a = a + dpp_x<1>(a);
+    a = a + dpp_x<2>(a);
+    double r = __shfl(a, 0, GW);
+#pragma unroll
+    for (int i = 8; i < 16; i++) {
+      const double x = __shfl(v, i % GW, GW);
+      r = (n < 16 && i < n) ? r + x : r;
+    }
+    return r;
+  }
+}
+
+// step_b waves per SIMD the register budget is sized for: 5 (<= 96 VGPRs) leaves room on each SIMD
+// for a demand-kernel wave of the next step next to the four step_b waves of this one
+#ifndef MSC_SB_WPE
+#define MSC_SB_WPE 5
+#endif
+
 // a wave-uniform double kept in scalar registers
 __device__ __forceinline__ double sgpr_d(double v) {
   const uint64_t b = (uint64_t)__double_as_longlong(v);
@@ -2072,7 +2112,7 @@ __device__ __forceinline__ double sgpr_d(double v) {
 }
 
 template <int K, int GW, bool DBG, bool TAB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int W = c.W, WK = W * K, R = c.R;
@@ -2215,10 +2255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
         const double lg = wl ? -(cof * (double)lost_cnt + cov * lw) / alpha : -INFINITY;
         const double mx = group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
         const double ex = wl ? exp(lg - mx) : 0.0;
-        double all[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) all[j] = j < GW ? __shfl(ex, j, GW) : 0.0;
-        wt = wl ? ex / np_sum_f64_16(all, W) : 0.0;
+        wt = wl ? ex / group_np_sum<GW>(ex, W) : 0.0;
       }
       // (a closest-warehouse share is 1.0 and 1.0 * x == x: one update form serves every type)
       if (wt != 0.0) {
@@ -2548,6 +2585,8 @@ static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st) 
     launch_split_demand<K, 3>(c, d, st);
   } else if (c.demand_gen == 4) {
     launch_split_demand<K, 4>(c, d, st);
+  } else if (c.demand_gen == 7) {
+    launch_split_demand<K, 7>(c, d, st);
   } else {
     launch_split_demand<K, 2>(c, d, st);
   }
