@@ -2288,6 +2288,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
 
   constexpr int NP = (K + 1) / 2;  // 32-bit words of a packed (16-bit per SKU) fill vector
   const int myjj = lane / GW;      // this group's env slot in the window
+  PROF_DECL(q_all);
+  PROF_DECL(q_fin);
+  PROF_DECL(q_alloc);
+  PROF_DECL(q_iter);
+  PROF_DECL(q_nfin);
+  PROF_T(q_t0);
   for (int oi = 0; oi <= wmax; oi++) {
     if (oi > 0 && oi % CH == 0) {  // wave-uniform: window oi / CH is due, start the one after
       if (oi + CH <= wmax) {
@@ -2312,7 +2318,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
       for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
     }
     if (r != cur) {
+      PROF_T(q_f0);
       if (cur >= 0) finalize(cur);
+      PROF_ADD(q_fin, PROF_NOW() - q_f0);
+      PROF_ADD(q_nfin, 1);
       if (r >= 0 && wl) {
         cof = cost_of(r);
         cov = cost_ov(r);
@@ -2341,7 +2350,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
     const uint64_t ckey = cbits ^ ((uint64_t)((int64_t)cbits >> 63) | 0x8000000000000000ull);
     int used = 0;
     bool open = true;
+    PROF_T(q_a0);
     while (open) {
+      PROF_ADD(q_iter, 1);
       // a warehouse that shipped already has nothing left that the order still needs
       // (fill = min(rem, inv) zeroes one of the two for every SKU), so "has" alone excludes it
       bool has = false;
@@ -2406,6 +2417,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
       used++;
       open = !done && used < maxwh;
     }
+    PROF_ADD(q_alloc, PROF_NOW() - q_a0);
     bool anyrem = false;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
@@ -2414,6 +2426,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
     }
     lost_cnt += anyrem ? 1 : 0;
   }
+  PROF_ADD(q_all, PROF_NOW() - q_t0);
+  PROF_FLUSH(10, q_all);
+  PROF_FLUSH(11, q_fin);
+  PROF_FLUSH(12, q_alloc);
+  PROF_FLUSH(13, q_iter);
+  PROF_FLUSH(14, q_nfin);
+  PROF_FLUSH(15, 1ull);
   if (ev && wl) {
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {

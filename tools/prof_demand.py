@@ -52,5 +52,5 @@ print(f"cycles per settle {v[1]/max(v[3],1):.0f}; per round (excl settles) {(v[0
 gw = max(waves, 1) * int(os.environ.get("GEN", "2"))
 print(f"generator cycles/wave: gen {v[8]/N/gw:.0f}  barrier {v[9]/N/gw:.0f}")
 sw = max(v[15] / N, 1)
-print(f"step kernel cycles/wave: order loop {v[10]/N/sw:.0f}  finalize {v[11]/N/sw:.0f}  allocation {v[12]/N/sw:.0f}  "
-      f"iterations {v[13]/N/sw:.0f}  finalize passes {v[14]/N/sw:.0f}")
+print(f"step_b cycles/wave: order loop {v[10]/N/sw:.0f}  region epilogues {v[11]/N/sw:.0f}  allocation {v[12]/N/sw:.0f}  "
+      f"allocation iterations (lane 0) {v[13]/N/sw:.0f}  epilogue passes {v[14]/N/sw:.0f}")
