@@ -213,31 +213,18 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   }
   c.order_cap = order_cap;
   {
-    const char* abl = getenv("MSC_ABLATE");
-    c.ablate = abl ? atoi(abl) : 0;
+    // A/B knobs (timing experiments only; results are identical)
     const char* impl = getenv("MSC_DEMAND_IMPL");
-    c.demand_impl = !impl ? 0
-                    : strcmp(impl, "nested") == 0       ? 1
-                    : strcmp(impl, "flat_branchy") == 0 ? 2
-                    : strcmp(impl, "flat") == 0         ? 3
-                    : strcmp(impl, "park1") == 0        ? 4
-                    : strcmp(impl, "park4") == 0        ? 5
-                                                        : 0;
+    c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : 0;
     const char* gen = getenv("MSC_DEMAND_GEN");
-    c.demand_gen = gen && ((atoi(gen) >= 1 && atoi(gen) <= 4) || atoi(gen) == 7) ? atoi(gen) : 3;
-    auto epw = [](const char* name, int dflt) {
-      const char* v = getenv(name);
-      const int x = v ? atoi(v) : dflt;
-      return x == 16 || x == 32 || x == 64 ? x : dflt;
-    };
-    c.epw_dem = epw("MSC_DEMAND_EPW", 64);
+    c.demand_gen = gen && atoi(gen) >= 1 && atoi(gen) <= 3 ? atoi(gen) : 3;
+    const char* v = getenv("MSC_DEMAND_EPW");
+    const int x = v ? atoi(v) : 64;
+    c.epw_dem = x == 16 || x == 32 || x == 64 ? x : 64;
     const char* pm = getenv("MSC_PARK_MIN");
     c.park_min = pm && atoi(pm) >= 1 && atoi(pm) <= 64 ? atoi(pm) : 32;
     const char* prot = getenv("MSC_PARSER_ROT");
     c.parser_rot = prot ? atoi(prot) : 0;
-    c.epw_step = epw("MSC_STEP_EPW", 64);
-    const char* si = getenv("MSC_STEP_IMPL");
-    c.step_impl = si && strcmp(si, "lane") == 0 ? 1 : 0;
   }
 
   TablePack tp;
@@ -398,10 +385,6 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   // stage the outbound cost table in LDS only when two blocks of each still fit one CU's LDS.
   // Otherwise the step kernel's blocks wait for the demand kernel's and nothing overlaps
   // (measured: 3.4 -> 2.2 ms per step at 8x64x5 with the table in global memory).
-  c.cost_lds = 2 * (step_lds_bytes_for(c, true) + demand_lds_bytes(c)) <= LDS_BUDGET ? 1 : 0;
-  if (const char* v = getenv("MSC_COST_LDS")) c.cost_lds = atoi(v) != 0 && step_lds_bytes_for(c, true) <= LDS_BUDGET;
-  c.dem_lds = (size_t)(2 + K) * R * sizeof(double) <= 64 * 1024 ? 1 : 0;
-  if (step_lds_bytes(c) > LDS_BUDGET) return fail(set_err(-1, "W*K too large for the LDS budget"));
   env->c = c;
   env->s = s;
   {

@@ -28,16 +28,11 @@ struct EnvConst {
   int32_t W, K, R, T, Lmax, RING, F, L, order_cap;
   int32_t action_type, lead_type, dev_per_sku, lost_type, scope, norm, wid, num_eval, max_wh;
   int32_t demand_type, init_type, init_min, init_max, hold_per_sku, pen_per_sku, tr_rows;
-  int32_t cost_lds;     // 1: step kernel stages the [R][W] outbound cost tables in LDS
-  int32_t dem_lds;      // 1: demand kernel stages the Poisson rate tables in LDS
-  int32_t ablate;       // timing-only phase ablation bits (MSC_ABLATE env var); 0 in production
-  int32_t demand_impl;  // 0 = generator waves + unit-per-round parser (default); A/B: 1 nested, 2 flat_branchy, 3 flat, 4 park1, 5 park4
+  int32_t demand_impl;  // 0 = generator waves + unit-per-round parser (default); 5 = park4 (A/B)
   int32_t demand_gen;   // generator waves per block of the split demand kernel (1, 2 or 3)
   int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
   int32_t parser_rot;   // which wave of a demand block parses: (wave + rot(block)) % (1 + G) == 0 (A/B knob)
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
-  int32_t epw_step;     // envs per 64-lane block of the lane-per-env step kernel (A/B only)
-  int32_t step_impl;    // 0 = group-per-env step kernel (default), 1 = lane-per-env (MSC_STEP_IMPL=lane)
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;
@@ -106,19 +101,6 @@ struct StepIO {
 
 constexpr uint32_t ERR_ORDER_OVERFLOW = 1u;
 
-// int32 words of the step kernel's per-lane LDS arrays (inventory, shipped-to-region,
-// shipped-total, shipped-home: 4*W*K), rounded to 16 B.
-__host__ __device__ inline int step_lds_ints(const EnvConst& c) {
-  const int n = (4 * c.W * c.K) * BS;
-  return (n + 3) & ~3;
-}
-// total dynamic LDS of the step kernel, with or without the shared outbound cost table
-inline size_t step_lds_bytes_for(const EnvConst& c, bool cost_table) {
-  return (size_t)step_lds_ints(c) * 4 + (size_t)3 * c.W * BS * sizeof(double) +
-         (cost_table ? (size_t)2 * c.R * c.W * sizeof(double) + (size_t)2 * c.R * sizeof(int32_t) : 0);
-}
-constexpr size_t LDS_BUDGET = 160 * 1024;
-
 // launchers (env_kernels.hip)
 // The descriptor + state pointers live in device memory and kernels take a pointer to them:
 // fields are then scalar-cache loads, and no address-taken kernel argument is copied to scratch.
@@ -132,7 +114,6 @@ hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask,
 hipError_t launch_step(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen_demand, hipStream_t st);
 hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st);
 hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hipStream_t st);
-size_t step_lds_bytes(const EnvConst& c);
 size_t demand_lds_bytes(const EnvConst& c);  // per block of the production demand kernel
 int order_record_vec4(int K);
 // gae.hip

@@ -1,15 +1,13 @@
 // env_kernels.hip -- HIP kernels of the vectorised InventoryEnvironment (gfx950 / CDNA4).
 //
-// One lane = one environment. A step is two launches on the caller's stream:
-//   1. demand_poisson_kernel  PoissonDemandSampler.sample   (demand_sampler.py:105-163)
-//      draws every order of the step from the env's own PCG64 stream into a per-step order
-//      buffer (records [slot][E], 16 B each), region-major exactly like the reference's list.
-//   2. step_kernel            InventoryEnvironment.step     (multi_env.py:253-366)
-//      rescale actions, lead times, orders/arrivals (phase A, coalesced over (w,s)),
-//      greedy allocation streamed region by region with the lost-sales epilogue folded into
-//      each region change (phase B, per-lane LDS for the (warehouse, SKU) arrays that the
-//      cost ranking indexes dynamically), then inventory/history/forecast, rewards and the
-//      per-agent observations (phase C), and an in-kernel reset when the episode truncates.
+// A step is four launches on the caller's stream:
+//   1. demand_unit_kernel  PoissonDemandSampler.sample (demand_sampler.py:105-163): generator
+//      waves + a one-unit-per-round parser draw every order of the step from the env's own
+//      PCG64 stream into a per-step order buffer (records [slot][E], 16 B each), region-major
+//      exactly like the reference's list;
+//   2-4. step_a / step_b / step_c  InventoryEnvironment.step (multi_env.py:253-366): actions,
+//      lead times, orders and arrivals; the greedy allocation with the lost-sales epilogue;
+//      inventory/history/forecast, rewards, observations and the in-kernel reset at truncation.
 // Integer state is exact; f32 observation arithmetic follows numpy's dtype flow operation by
 // operation (the library is built with -ffp-contract=off so no FMA contraction changes a
 // rounding); rewards are f64.
@@ -388,351 +386,10 @@ __global__ __launch_bounds__(BS) void reset_kernel(const DevEnv* __restrict__ dp
 // latency hides under the following PCG64 draw. No branch except the order-record store.
 constexpr int PS_MASK = 0, PS_ORD = 1, PS_QTY = 2, PS_DONE = 3;
 
-template <int K, bool LDS_TAB>
-__global__ __launch_bounds__(BS) void demand_flat_kernel(const DevEnv* __restrict__ dp) {
-  const EnvConst& c = dp->c;
-  const EnvState& s = dp->s;
-  const int R = c.R;
-  extern __shared__ __attribute__((aligned(16))) double tlds[];
-  const double* To = c.enlam_o;  // [R]
-  const double* Tp = c.p_sku;    // [R]
-  const double* Tq = c.enlam_q;  // [R*K]
-  if constexpr (LDS_TAB) {
-    double* lo = tlds;
-    double* lp = tlds + R;
-    double* lq = tlds + 2 * R;
-    for (int i = threadIdx.x; i < R; i += BS) {
-      lo[i] = c.enlam_o[i];
-      lp[i] = c.p_sku[i];
-    }
-    for (int i = threadIdx.x; i < R * K; i += BS) lq[i] = c.enlam_q[i];
-    __syncthreads();
-    To = lo;
-    Tp = lp;
-    Tq = lq;
-  }
-  const int64_t e = (int64_t)blockIdx.x * c.epw_dem + threadIdx.x;
-  if ((int)threadIdx.x >= c.epw_dem || e >= c.E) return;
-  const int64_t E = c.E;
-  constexpr int NV = Rec<K>::NV;
-  constexpr int NW = 2 * NV;
-  Pcg64 rg = load_rng(s, 0, e, E);
-  store_rng_pre(s, e, E, rg);
-  int st = PS_ORD, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0;
-  unsigned mask = 0;
-  double prod = 1.0, thr = To[0], p = Tp[0];
-  uint64_t rec[NW];
-#pragma unroll
-  for (int j = 0; j < NW; j++) rec[j] = 0;
-  // prefetched for the next pass
-  double pre_o = To[R > 1 ? 1 : 0], pre_p = Tp[R > 1 ? 1 : 0], pre_q = Tq[0];
-  MSC_GLOBAL uint4* out = gp(s.orders + e);
-  const int cap = c.order_cap;
-  while (st != PS_DONE) {
-    const double U = pcg_double(rg);
-    // ---- consume the draw
-    const bool in_mask = st == PS_MASK;
-    const double prod_u = prod * U;
-    const bool cont = prod_u > thr;
-    const unsigned mask_u = mask | ((U < p) ? (1u << k) : 0u);
-    const bool ev_maskdone = in_mask && (k + 1 == K);
-    const bool ev_done = !in_mask && !cont;
-    const bool ev_region = ev_done && st == PS_ORD;
-    const bool ev_qty = ev_done && st == PS_QTY;
-    mask = in_mask ? mask_u : mask;
-    k = in_mask ? k + 1 : k;
-    prod = in_mask ? prod : prod_u;
-    x = (!in_mask && cont) ? x + 1 : x;
-    // ---- settle: quantity of the current SKU, then next SKU or emit, then next order/region
-    {
-      const uint64_t v = (uint64_t)(x > 1 ? x : 1);
-      const int sh = 16 * (1 + sq);
-#pragma unroll
-      for (int j = 0; j < NW; j++) rec[j] |= (ev_qty && (sh >> 6) == j) ? v << (sh & 63) : 0;
-    }
-    mask = ev_qty ? (mask & (mask - 1u)) : mask;
-    const bool next_sku = ev_maskdone || ev_qty;
-    const bool start_q = next_sku && mask != 0;
-    const bool emit = next_sku && mask == 0;
-    sq = start_q ? __builtin_ctz(mask) : sq;
-    left = ev_region ? x : left;
-    if (emit && n < cap) {
-#pragma unroll
-      for (int j = 0; j < NV; j++)
-        gstore4(out, ((int64_t)n * NV + j) * E,
-                make_uint4((uint32_t)rec[2 * j], (uint32_t)(rec[2 * j] >> 32), (uint32_t)rec[2 * j + 1],
-                           (uint32_t)(rec[2 * j + 1] >> 32)));
-    }
-    n += emit ? 1 : 0;
-    left -= emit ? 1 : 0;
-    const bool next_order = emit || ev_region;
-    const bool start_order = next_order && left > 0;
-    const bool next_region = next_order && left == 0;
-    const bool done = next_region && r + 1 == R;
-    const bool start_region = next_region && !done;
-    r = start_region ? r + 1 : r;
-#pragma unroll
-    for (int j = 0; j < NW; j++) rec[j] = start_order ? (j == 0 ? (uint64_t)r : 0) : rec[j];
-    mask = start_order ? 0u : mask;
-    k = start_order ? 0 : k;
-    thr = start_q ? pre_q : (start_region ? pre_o : thr);
-    p = start_region ? pre_p : p;
-    prod = (start_q || start_region) ? 1.0 : prod;
-    x = (start_q || start_region) ? 0 : x;
-    st = done ? PS_DONE : start_region ? PS_ORD : start_order ? PS_MASK : start_q ? PS_QTY : st;
-    // ---- prefetch what the next pass may need
-    const unsigned nm = mask & (mask - 1u);
-    const int cand = st == PS_QTY ? (nm ? __builtin_ctz(nm) : 0) : (mask ? __builtin_ctz(mask) : K - 1);
-    const int rn = r + 1 < R ? r + 1 : r;
-    pre_q = Tq[r * K + cand];
-    pre_o = To[rn];
-    pre_p = Tp[rn];
-  }
-  store_rng(s, 0, e, E, rg);
-  if (n > cap) {
-    atomicOr(s.err, ERR_ORDER_OVERFLOW);
-    n = cap;
-  }
-  s.n_orders[e] = n;
-}
-
 // ------------------------------------------------------------------------------------------
-// Production demand kernel: generator waves + a parking parser.
-//
-// Measured on gfx950 (tools/ubench_rng.hip): one PCG64 draw costs ~88 ns per wave, but the flat
-// kernel above spends ~450 ns per draw, ~80 % of it in the sampler's state machine, which runs for
-// every lane on every draw because some lane of the 64 always changes state. Here a block owns
-// 64 envs with 1 + G waves:
-//   * generator waves 1..G advance each lane's PCG64 stream and write its uniforms into a
-//     per-lane LDS ring [DCAP][64] indexed by stream position (generator g of G writes positions
-//     g, g+G, ... using the G-step affine map of pcg_jump_coeffs);
-//   * the parser wave 0 splits the sampler into units that consume draws -- a Poisson loop
-//     (orders of a region, or one SKU quantity) or the K Bernoulli draws of an order's SKU mask --
-//     and the zero-draw bookkeeping between units. The hot loop only advances the current unit
-//     (prod *= U; compare; count) and PARKS a lane whose unit ended; once >= park_min lanes (or
-//     all live lanes) are parked, one settle pass handles all of them: record the quantity, emit
-//     the order, open the next SKU / order / region unit. The Bernoulli test U < p is folded into
-//     the same comparison (U > p_skip, prod = 1 in the mask unit).
-// Chunks of DCH hot iterations (each lane consumes <= 1 draw per iteration) are separated by one
-// barrier at which the parser publishes every lane's consumed count; the generators then refill
-// each lane's ring up to consumed + DCAP, which never touches a position the parser can still read
-// in the next chunk. The final stream state is the start state advanced by the consumed count.
-// ------------------------------------------------------------------------------------------
-#ifndef MSC_DCH
-#define MSC_DCH 16
-#endif
-constexpr int DCH = MSC_DCH;   // hot iterations per chunk
-constexpr int DCAP = 2 * DCH;  // per-lane ring capacity (draws)
-
-__host__ __device__ constexpr size_t park_lds_fixed() {
-  return (size_t)DCAP * BS * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
-}
-
-template <int K, int G, bool LDS_TAB>
-__global__ __launch_bounds__(BS * (1 + G)) void demand_park_kernel(const DevEnv* __restrict__ dp) {
-  const EnvConst& c = dp->c;
-  const EnvState& s = dp->s;
-  const int R = c.R;
-  constexpr int NV = Rec<K>::NV;
-  constexpr int NW = 4 * NV;  // 32-bit words of an order record
-  extern __shared__ __attribute__((aligned(16))) double plds[];
-  __shared__ int more[2];
-  double* ring = plds;                                           // [DCAP][BS]
-  int32_t* rdv = reinterpret_cast<int32_t*>(plds + DCAP * BS);   // [2][BS] consumed draws per lane
-  const double* To = c.enlam_o;
-  const double* Tk = c.p_skip;
-  const double* Tq = c.enlam_q;
-  if constexpr (LDS_TAB) {
-    double* lo = plds + DCAP * BS + BS;  // after rdv (2*BS int32 = BS doubles)
-    double* lk = lo + R;
-    double* lq = lk + R;
-    for (int i = threadIdx.x; i < R; i += blockDim.x) {
-      lo[i] = c.enlam_o[i];
-      lk[i] = c.p_skip[i];
-    }
-    for (int i = threadIdx.x; i < R * K; i += blockDim.x) lq[i] = c.enlam_q[i];
-    To = lo;
-    Tk = lk;
-    Tq = lq;
-  }
-  const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;  // role is wave-uniform
-  const int64_t E = c.E;
-  const int64_t e = (int64_t)blockIdx.x * c.epw_dem + lane;
-  const bool valid = lane < c.epw_dem && e < E;
-
-  if (wave > 0) {
-    // ---------------- generator g: stream positions g, g + G, g + 2G, ...
-    const int g = wave - 1;
-    uint64_t th = 0, tl = 0, ih = 0, il = 1;
-    if (valid) {
-      Pcg64 rg = load_rng(s, 0, e, E);
-      for (int j = 0; j <= g; j++) pcg_step(rg);  // the state whose output is draw g
-      th = rg.s_hi;
-      tl = rg.s_lo;
-      ih = rg.i_hi;
-      il = rg.i_lo;
-    }
-    uint64_t mh = PCG_MUL_HI, ml = PCG_MUL_LO, ch = ih, cl = il;
-    if constexpr (G > 1) pcg_jump_coeffs(G, ih, il, mh, ml, ch, cl);
-    int pg = g;
-    auto gen_to = [&](int target) {
-      while (pg < target) {
-        ring[(pg & (DCAP - 1)) * BS + lane] = u64_to_double(pcg_output(th, tl));
-        uint64_t nh, nl;
-        mul128(th, tl, mh, ml, nh, nl);
-        add128(nh, nl, ch, cl);
-        th = nh;
-        tl = nl;
-        pg += G;
-      }
-    };
-    PROF_DECL(p_gen);
-    PROF_DECL(p_bar);
-    if (valid) gen_to(DCAP);
-    __syncthreads();
-    for (int ci = 0;; ci++) {
-      PROF_T(t0);
-      if (valid) gen_to(rdv[(ci & 1) * BS + lane] + DCAP);
-      PROF_T(t1);
-      __syncthreads();
-      PROF_ADD(p_gen, t1 - t0);
-      PROF_ADD(p_bar, PROF_NOW() - t1);
-      if (!more[ci & 1]) break;
-    }
-    PROF_FLUSH(8, p_gen);
-    PROF_FLUSH(9, p_bar);
-    return;
-  }
-
-  // ---------------- parser
-  Pcg64 r0{};
-  if (valid) {
-    r0 = load_rng(s, 0, e, E);
-    store_rng_pre(s, e, E, r0);
-  }
-  rdv[lane] = 0;
-  int st = valid ? PS_ORD : PS_DONE, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0, rd = 0;
-  unsigned mask = 0;
-  int pk = 0, mf = 0, live = valid ? 1 : 0;  // parked / unit is the SKU mask / not done (0 or 1)
-  uint32_t w[NW];
-#pragma unroll
-  for (int j = 0; j < NW; j++) w[j] = 0;
-  const int cap = c.order_cap;
-  const int pmin = c.park_min;
-  MSC_GLOBAL uint4* out = gp(s.orders + e);
-  __syncthreads();  // tables and the first DCAP draws of every lane are in LDS
-  double prod = 1.0, thr = To[0];
-  // settle pass over the parked lanes (branch-free apart from the record store): the lane's unit
-  // ended; book its result and open the next unit that consumes draws
-  auto settle = [&]() {
-    const bool is_ord = st == PS_ORD, is_qty = st == PS_QTY;
-    const uint32_t v = (uint32_t)(x > 1 ? x : 1);  // max(1, Poisson(lambda_q))
-    const int h = 1 + sq;
-#pragma unroll
-    for (int j = 0; j < NW; j++) w[j] |= (is_qty && (h >> 1) == j) ? v << (16 * (h & 1)) : 0u;
-    mask = is_qty ? (mask & (mask - 1u)) : mask;
-    const int nsq = mask ? __builtin_ctz(mask) : 0;
-    const int rn = r + 1 < R ? r + 1 : r;
-    const double q_thr = Tq[r * K + nsq], k_thr = Tk[r], o_thr = To[rn];  // speculative, one latency
-    const bool start_q = !is_ord && mask != 0;
-    const bool emit = !is_ord && mask == 0;  // order complete (possibly without SKUs)
-    if (emit && n < cap) {
-#pragma unroll
-      for (int j = 0; j < NV; j++)
-        gstore4(out, ((int64_t)n * NV + j) * E, make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]));
-    }
-    n += emit ? 1 : 0;
-    left = is_ord ? x : left - (emit ? 1 : 0);  // region r: Poisson(lambda_orders) orders
-    const bool start_order = !start_q && left > 0;
-    const bool next_region = !start_q && left <= 0;
-    const bool start_region = next_region && r + 1 < R;
-    r += start_region ? 1 : 0;
-    sq = start_q ? nsq : sq;
-    st = start_q ? PS_QTY : start_order ? PS_MASK : start_region ? PS_ORD : PS_DONE;
-    thr = start_q ? q_thr : start_order ? k_thr : o_thr;
-    mask = start_order ? 0u : mask;
-#pragma unroll
-    for (int j = 0; j < NW; j++) w[j] = start_order ? (j == 0 ? (uint32_t)r : 0u) : w[j];
-    prod = 1.0;
-    x = 0;
-    k = 0;
-    pk = 0;
-    mf = st == PS_MASK ? 1 : 0;
-    live = st != PS_DONE ? 1 : 0;
-  };
-  constexpr int Q = 4;  // draws read per lane per round (one LDS latency per round)
-  PROF_DECL(p_all);
-  PROF_DECL(p_set);
-  PROF_DECL(p_bar);
-  PROF_DECL(n_set);
-  PROF_DECL(n_round);
-  PROF_DECL(n_chunk);
-  PROF_T(t_start);
-  for (int ci = 0;; ci++) {
-    for (int rr = 0; rr < DCH / Q; rr++) {
-      double u[Q];
-#pragma unroll
-      for (int j = 0; j < Q; j++) u[j] = ring[((rd + j) & (DCAP - 1)) * BS + lane];
-      int cr = 0;  // draws this lane consumed in the round
-#pragma unroll
-      for (int j = 0; j < Q; j++) {
-        // ---- hot: advance the lane's current unit by one draw. Flags are 0/1 integers combined
-        // with VALU bit operations: SGPR lane-mask logic and exec branches (VCC -> SALU -> exec
-        // round trips) cost more than the arithmetic itself here.
-        double U = u[0];
-#pragma unroll
-        for (int m = 1; m <= j; m++) U = cr == m ? u[m] : U;
-        const int a = live & (pk ^ 1);  // lane consumes this draw
-        const double pu = prod * U;
-        const int ct = pu > thr ? 1 : 0;  // Poisson: product above exp(-lambda); mask: SKU not drawn
-        const int am = a & mf, ap = a & (mf ^ 1);
-        mask |= (unsigned)(am & (ct ^ 1)) << k;
-        k += am;
-        const int pc = ap & ct;
-        x += pc;
-        prod = pc ? pu : prod;
-        pk |= (am & ((k + (64 - K)) >> 6)) | (ap & (ct ^ 1));  // mask: k == K; Poisson: ended
-        cr += a;
-        const uint64_t pkm = __ballot(pk);
-        if (pkm != 0 && (__popcll(pkm) >= pmin || pkm == __ballot(live))) {
-          PROF_T(ts);
-          if (pk) settle();
-          PROF_ADD(p_set, PROF_NOW() - ts);
-          PROF_ADD(n_set, 1);
-        }
-      }
-      rd += cr;
-      PROF_ADD(n_round, 1);
-    }
-    const bool any = __ballot(st != PS_DONE) != 0;
-    rdv[((ci + 1) & 1) * BS + lane] = rd;
-    if (lane == 0) more[ci & 1] = any ? 1 : 0;
-    PROF_T(tb);
-    __syncthreads();
-    PROF_ADD(p_bar, PROF_NOW() - tb);
-    PROF_ADD(n_chunk, 1);
-    if (!any) break;
-  }
-  PROF_ADD(p_all, PROF_NOW() - t_start);
-  PROF_FLUSH(0, p_all);
-  PROF_FLUSH(1, p_set);
-  PROF_FLUSH(2, p_bar);
-  PROF_FLUSH(3, n_set);
-  PROF_FLUSH(4, n_round);
-  PROF_FLUSH(5, n_chunk);
-  PROF_FLUSH(6, 1ull);
-  if (!valid) return;
-  pcg_advance(r0, (uint64_t)rd);
-  store_rng(s, 0, e, E, r0);
-  if (n > cap) {
-    atomicOr(s.err, ERR_ORDER_OVERFLOW);
-    n = cap;
-  }
-  s.n_orders[e] = n;
-}
-
-// ------------------------------------------------------------------------------------------
-// demand_park4_kernel: the parking parser with multi-draw hot steps (production default).
+// demand_park4_kernel: the parking parser with multi-draw hot steps (A/B baseline of
+// demand_unit_kernel: MSC_DEMAND_IMPL=park4). Generators as in demand_unit_kernel; the parser parks
+// a lane whose unit ended and settles parked lanes in batches of >= park_min.
 //
 // Same generator / parser split and settle pass as demand_park_kernel, but one hot step advances
 // a lane's unit by up to PD = 4 draws at once: the Poisson products p1..p4 are chained
@@ -996,7 +653,6 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   const EnvState& s = dp->s;
   const int R = c.R;
   constexpr int NV = Rec<K>::NV;
-  constexpr int NW = 4 * NV;
   extern __shared__ __attribute__((aligned(16))) double plds[];
   __shared__ int more[2];
   double* ring = plds;                                             // [USLOTS][BS]
@@ -1188,706 +844,6 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     n = cap;
   }
   s.n_orders[e] = n;
-}
-
-// Variant with branchy settling (kept for A/B measurement: MSC_DEMAND_IMPL=flat_branchy).
-//
-// The reference's draw sequence per step is: for each region, Poisson(lambda_o) (multiplication
-// method: uniforms until the running product drops to exp(-lambda)); per order K uniforms for the
-// Bernoulli SKU mask; per selected SKU (ascending) max(1, Poisson(lambda_q)). Written as nested
-// loops, the 64 lanes of a wave re-converge at every region/order/SKU boundary and wait for the
-// slowest lane each time (~7x wasted issue). Here every loop iteration draws exactly one uniform
-// per active lane and advances that lane's own parser; the zero-draw transitions (region done,
-// empty order, order emitted) are settled per lane before the next draw. A wave therefore runs
-// for max-over-lanes of the TOTAL draws per step (~6.7k at 8x64x5, within ~15% of the mean).
-enum : int { ST_MASK = 0, ST_POIS = 1, ST_REGION = 2, ST_ORDERS = 3, ST_MASKDONE = 4, ST_QSTART = 5, ST_QNEXT = 6, ST_DONE = 7 };
-
-template <int K>
-__global__ __launch_bounds__(BS) void demand_poisson_kernel(const DevEnv* __restrict__ dp) {
-  const EnvConst& c = dp->c;
-  const EnvState& s = dp->s;
-  // rate tables in LDS: each lane gathers its own region's thresholds on every settle
-  extern __shared__ __attribute__((aligned(16))) double dlds[];
-  double* Lo = dlds;            // [R]   exp(-lambda_orders)
-  double* Lp = dlds + c.R;      // [R]   probability_skus
-  double* Lq = dlds + 2 * c.R;  // [R*K] exp(-lambda_quantity)
-  const bool tl = c.dem_lds != 0;
-  if (tl) {
-    for (int i = threadIdx.x; i < c.R; i += BS) {
-      Lo[i] = c.enlam_o[i];
-      Lp[i] = c.p_sku[i];
-    }
-    for (int i = threadIdx.x; i < c.R * K; i += BS) Lq[i] = c.enlam_q[i];
-    __syncthreads();
-  }
-  const int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x;
-  if (e >= c.E) return;
-  const int64_t E = c.E;
-  const int R = c.R;
-  constexpr int NV = Rec<K>::NV;
-  constexpr int NW = 2 * NV;  // 64-bit words of a record
-  Pcg64 rg = load_rng(s, 0, e, E);
-  store_rng_pre(s, e, E, rg);
-  int st = ST_REGION, r = 0, x = 0, k = 0, left = 0, sq = 0, n = 0;
-  bool isq = false;
-  unsigned mask = 0;
-  double prod = 1.0, thr = 0.0, p = 0.0;
-  uint64_t rec[NW];
-#pragma unroll
-  for (int j = 0; j < NW; j++) rec[j] = 0;
-  uint4* out = s.orders + e;
-  for (;;) {
-    // Settle the transitions that consume no draw, in their natural order, as one straight-line
-    // pass (a chain qty-done -> emit -> next order / next region completes in one pass; only a
-    // zero-rate quantity or region repeats it).
-    while (st >= ST_REGION && st != ST_DONE) {
-      if (st == ST_MASKDONE) {
-        if (mask) {
-          sq = __builtin_ctz(mask);
-          st = ST_QSTART;
-        } else {
-          st = ST_QNEXT;
-        }
-      }
-      if (st == ST_QSTART) {
-        thr = tl ? Lq[r * K + sq] : c.enlam_q[r * K + sq];
-        if (thr >= 1.0) {  // lambda == 0: Poisson -> 0 without a draw, quantity max(1, 0)
-          const int sh = 16 * (1 + sq);
-#pragma unroll
-          for (int j = 0; j < NW; j++) rec[j] |= (sh >> 6) == j ? (uint64_t)1 << (sh & 63) : 0;
-          mask &= mask - 1u;
-          st = mask ? ST_MASKDONE : ST_QNEXT;
-        } else {
-          prod = 1.0; x = 0; isq = true; st = ST_POIS;
-        }
-      }
-      if (st == ST_QNEXT) {  // every selected SKU drawn: emit the order
-        if (n < c.order_cap) {
-          uint4* dst = out + (int64_t)n * NV * E;
-#pragma unroll
-          for (int j = 0; j < NV; j++)
-            dst[j * E] = make_uint4((uint32_t)rec[2 * j], (uint32_t)(rec[2 * j] >> 32), (uint32_t)rec[2 * j + 1],
-                                    (uint32_t)(rec[2 * j + 1] >> 32));
-        }
-        n++;
-        left--;
-        st = ST_ORDERS;
-      }
-      if (st == ST_ORDERS) {
-        if (left == 0) {
-          r++;
-          st = ST_REGION;
-        } else {
-          mask = 0; k = 0; st = ST_MASK;
-#pragma unroll
-          for (int j = 0; j < NW; j++) rec[j] = 0;
-          rec[0] = (uint64_t)r;
-        }
-      }
-      if (st == ST_REGION) {
-        if (r == R) {
-          st = ST_DONE;
-        } else {
-          thr = tl ? Lo[r] : c.enlam_o[r];
-          p = tl ? Lp[r] : c.p_sku[r];
-          if (thr >= 1.0) {  // lambda == 0: no orders, no draw
-            left = 0; st = ST_ORDERS;
-          } else {
-            prod = 1.0; x = 0; isq = false; st = ST_POIS;
-          }
-        }
-      }
-    }
-    if (st == ST_DONE) break;
-    const double U = pcg_double(rg);
-    if (st == ST_MASK) {
-      mask |= (U < p) ? (1u << k) : 0u;
-      if (++k == K) st = ST_MASKDONE;
-    } else {
-      prod *= U;
-      if (prod > thr) {
-        x++;
-      } else if (!isq) {
-        left = x;
-        st = ST_ORDERS;
-      } else {
-        const uint64_t v = (uint64_t)(x > 1 ? x : 1);
-        const int sh = 16 * (1 + sq);
-#pragma unroll
-        for (int j = 0; j < NW; j++) rec[j] |= (sh >> 6) == j ? v << (sh & 63) : 0;
-        mask &= mask - 1u;
-        st = mask ? ST_MASKDONE : ST_QNEXT;
-      }
-    }
-  }
-  store_rng(s, 0, e, E, rg);
-  if (n > c.order_cap) {
-    atomicOr(s.err, ERR_ORDER_OVERFLOW);
-    n = c.order_cap;
-  }
-  s.n_orders[e] = n;
-}
-
-// Reference-shaped nested-loop version (kept for A/B measurement; not launched).
-template <int K>
-__global__ __launch_bounds__(BS) void demand_poisson_nested_kernel(const DevEnv* __restrict__ dp) {
-  const EnvConst& c = dp->c;
-  const EnvState& s = dp->s;
-  const int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x;
-  if (e >= c.E) return;
-  const int64_t E = c.E;
-  constexpr int NV = Rec<K>::NV;
-  Pcg64 rg = load_rng(s, 0, e, E);
-  store_rng_pre(s, e, E, rg);
-  int n = 0;
-  for (int r = 0; r < c.R; r++) {
-    const double elo = c.enlam_o[r], p = c.p_sku[r];
-    const int no = elo >= 1.0 ? 0 : poisson_mult(rg, elo);
-    for (int k = 0; k < no; k++) {
-      unsigned mask = 0;
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) mask |= (pcg_double(rg) < p) ? (1u << sk) : 0u;
-      int q[K];
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) {
-        q[sk] = 0;
-        if (mask & (1u << sk)) {
-          const double el = c.enlam_q[r * K + sk];
-          int v = el >= 1.0 ? 0 : poisson_mult(rg, el);
-          q[sk] = v > 1 ? v : 1;
-        }
-      }
-      if (n < c.order_cap) store_rec<K>(s.orders + ((int64_t)n * E * NV) + e, E, r, q);
-      n++;
-    }
-  }
-  store_rng(s, 0, e, E, rg);
-  if (n > c.order_cap) {
-    atomicOr(s.err, ERR_ORDER_OVERFLOW);
-    n = c.order_cap;
-  }
-  s.n_orders[e] = n;
-}
-
-// compare-and-swap of (cost, warehouse) pairs: ascending cost, lowest index first on ties
-__device__ __forceinline__ void cas(double& ca, int& ia, double& cb, int& ib) {
-  const bool sw = (cb < ca) || (cb == ca && ib < ia);
-  const double tc = sw ? cb : ca;
-  const int ti = sw ? ib : ia;
-  cb = sw ? ca : cb;
-  ib = sw ? ia : ib;
-  ca = tc;
-  ia = ti;
-}
-template <int WM>
-__device__ __forceinline__ void sort_costs(double (&c)[WM], int (&ix)[WM]) {
-  // odd-even transposition network: WM rounds, fully unrolled (all indices static)
-#pragma unroll
-  for (int round = 0; round < WM; round++)
-#pragma unroll
-    for (int a = round & 1; a + 1 < WM; a += 2) cas(c[a], ix[a], c[a + 1], ix[a + 1]);
-}
-
-template <int K, int WM, bool TAB_LDS>
-__global__ __launch_bounds__(BS) void step_kernel(const DevEnv* __restrict__ dp, StepIO io) {
-  const EnvConst& c = dp->c;
-  const EnvState& s = dp->s;
-  extern __shared__ __attribute__((aligned(16))) int32_t lds[];
-  const int lane = threadIdx.x;
-  const int64_t e = (int64_t)blockIdx.x * c.epw_step + lane;
-  const int64_t E = c.E;
-  const int W = c.W, WK = W * K, R = c.R, RING = c.RING;
-  // LDS: per-lane [field][idx][lane] arrays, then the block-shared outbound cost table
-  const int ni = step_lds_ints(c);
-  int32_t* Linv = lds + lane;                 // [WK]  inventory
-  int32_t* Lqsr = lds + 1 * WK * BS + lane;   // [WK]  shipped to the current region
-  int32_t* Lsht = lds + 2 * WK * BS + lane;   // [WK]  shipped in total this step
-  int32_t* Lshh = lds + 3 * WK * BS + lane;   // [WK]  shipped to the home region
-  double* Lpen = reinterpret_cast<double*>(lds + ni) + lane;  // [W] penalty cost
-  double* Lout = Lpen + W * BS;                                // [W] outbound cost
-  double* Linb = Lout + W * BS;                                // [W] inbound cost
-  // block-shared per-region tables: [2][R][W] f64 outbound costs, [R] closest, [R] home mask
-  const double* OFt = c.ofT;
-  const double* OVt = c.ovT;
-  const int32_t* CLt = c.closest;
-  const uint32_t* HMt = c.home_mask;
-  if constexpr (TAB_LDS) {
-    double* Tcost = reinterpret_cast<double*>(lds + ni) + 3 * W * BS;
-    int32_t* Tcl = reinterpret_cast<int32_t*>(Tcost + 2 * R * W);
-    uint32_t* Thm = reinterpret_cast<uint32_t*>(Tcl + R);
-    for (int i = lane; i < R * W; i += BS) {
-      Tcost[i] = c.ofT[i];
-      Tcost[R * W + i] = c.ovT[i];
-    }
-    for (int i = lane; i < R; i += BS) {
-      Tcl[i] = c.closest[i];
-      Thm[i] = c.home_mask[i];
-    }
-    __syncthreads();
-    OFt = Tcost;
-    OVt = Tcost + R * W;
-    CLt = Tcl;
-    HMt = Thm;
-  }
-  if (lane >= c.epw_step || e >= c.E) return;
-  // outbound cost rows of the region being allocated, cached in registers at each region change
-  // (orders are region-major): the allocator's per-order costs need no table reads
-  double cof[WM], cov[WM];
-#pragma unroll
-  for (int w = 0; w < WM; w++) cof[w] = cov[w] = 0.0;
-  auto load_costs = [&](int r) {
-#pragma unroll
-    for (int w = 0; w < WM; w++) {
-      cof[w] = w < W ? OFt[r * W + w] : 0.0;
-      cov[w] = w < W ? OVt[r * W + w] : 0.0;
-    }
-  };
-  const msc_step_info info = io.info;
-  const bool dbg = io.has_info != 0;
-
-  const int t = s.t[e];
-  // ---- phase 0: state -> LDS --------------------------------------------------------------
-  for (int i = 0; i < WK; i++) {
-    const int v = s.inv[i * E + e];
-    Linv[i * BS] = v;
-    Lqsr[i * BS] = 0;
-    Lsht[i * BS] = 0;
-    Lshh[i * BS] = 0;
-    if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = v;
-  }
-  for (int w = 0; w < W; w++) {
-    Lpen[w * BS] = 0.0;
-    Lout[w * BS] = 0.0;
-  }
-  const bool stoch = c.lead_type == MSC_LEAD_STOCHASTIC;
-  if (stoch) {  // lead_time_sampler.sample(): all W*K deviations drawn every step (multi_env.py:866)
-    Pcg64 rl = load_rng(s, 1, e, E);
-    if (c.dev_per_sku) {  // np.column_stack of per-SKU draws: SKU-major order (lead_time_sampler.py:181-185)
-#pragma unroll
-      for (int sk = 0; sk < K; sk++)
-        for (int w = 0; w < W; w++)
-          Lqsr[(w * K + sk) * BS] = (int32_t)bounded_int(rl, -c.maxdev[sk], (int64_t)c.maxdev[sk] + 1);
-    } else {
-      for (int i = 0; i < WK; i++) Lqsr[i * BS] = (int32_t)bounded_int(rl, -c.maxdev[0], (int64_t)c.maxdev[0] + 1);
-    }
-    store_rng(s, 1, e, E, rl);
-  }
-
-  // ---- phase A: actions -> orders, lead times, pending ring, arrivals -----------------------
-  const int slot = t % RING;
-  for (int w = 0; w < W; w++) {
-    double inbF = 0.0, inbV = 0.0;
-#pragma unroll
-    for (int sk = 0; sk < K; sk++) {
-      const int i = w * K + sk;
-      const float a = io.actions[(e * W + w) * K + sk];
-      const int inc_old = s.inc[i * E + e];
-      int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
-      int pend = 0;
-      for (int jr = 0; jr < RING; jr++) pend += rq[jr * E];
-      // _rescale_actions_to_quantities (multi_env.py:795-848)
-      const double prm = c.act_param[sk];
-      double q;
-      if (c.action_type == MSC_ACTION_DIRECT) {
-        q = rint((double)((a + 1.0f) / 2.0f) * prm);
-        q = q < 0.0 ? 0.0 : (q > prm ? prm : q);
-      } else if (c.action_type == MSC_ACTION_DEMAND_CENTERED) {
-        q = rint(prm * (double)a) + (double)inc_old;
-        q = q < 0.0 ? 0.0 : q;
-      } else {
-        const double target = (double)((a + 1.0f) / 2.0f) * prm;
-        q = rint((target - (double)(float)inc_old) - (double)(float)pend);
-        q = q < 0.0 ? 0.0 : q;
-      }
-      const int qi = (int)q;
-      const int elt = c.elt[i];
-      int lact = elt;
-      if (stoch) {
-        lact = elt + Lqsr[i * BS];
-        lact = lact > 1 ? lact : 1;
-      }
-      // _apply_orders: the slot of order time t (its previous occupant arrived already)
-      rq[slot * E] = qi;
-      if (stoch) s.ring_l[((int64_t)i * RING + slot) * E + e] = (uint8_t)lact;
-      // _apply_arrivals: orders whose actual arrival == t
-      int inv = Linv[i * BS];
-      for (int jr = 0; jr < RING; jr++) {
-        if (jr == slot) continue;
-        const int qq = rq[jr * E];
-        if (qq == 0) continue;
-        int age = (t - jr) % RING;
-        if (age < 0) age += RING;
-        const int l = stoch ? (int)s.ring_l[((int64_t)i * RING + jr) * E + e] : elt;
-        if (l == age) {
-          inv += qq;
-          rq[jr * E] = 0;
-        }
-      }
-      Linv[i * BS] = inv;
-      s.inc[i * E + e] = 0;
-      if (qi > 0) inbF += c.inF[i];
-      inbV += ((double)qi * c.skw[sk]) * c.inV[i];
-      if (dbg) {
-        if (info.pending_total) info.pending_total[e * WK + i] = pend;
-        if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
-      }
-    }
-    Linb[w * BS] = inbF + inbV;
-  }
-  if (stoch)
-    for (int i = 0; i < WK; i++) Lqsr[i * BS] = 0;
-
-  // ---- phase B: greedy allocation (demand_allocator.py:118-217) + per-region epilogue ------
-  const MSC_GLOBAL uint4* src;
-  int64_t stride;
-  int n_orders;
-  if (c.demand_type == MSC_DEMAND_EMPIRICAL) {  // demand_sampler.py:227-241
-    int st0 = s.emp_start[e];
-    if (st0 < 0) {
-      Pcg64 rg = load_rng(s, 0, e, E);
-      st0 = (int)bounded_int(rg, 0, (int64_t)(c.tr_rows - c.T) + 1);
-      store_rng(s, 0, e, E, rg);
-      s.emp_start[e] = st0;
-    }
-    const int64_t row = st0 + (t % c.T);
-    const int64_t off = c.tr_off[row];
-    n_orders = (int)(c.tr_off[row + 1] - off);
-    src = gp(c.tr_rec + off * Rec<K>::NV);
-    stride = 1;
-  } else {
-    n_orders = s.n_orders[e];
-    src = gp(s.orders + e);
-    stride = E;
-  }
-  if (dbg && info.n_orders) info.n_orders[e] = n_orders;
-  const int64_t rec_step = stride * Rec<K>::NV;
-
-  int cur = -1, lost_cnt = 0;
-  unsigned touched = 0;
-  int u[K], dsum[K];
-#pragma unroll
-  for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
-
-  // region epilogue: lost sales (lost_sales_handler.py) folded into the penalty cost, the
-  // home-region features and, in diagnostic mode, the per-region infos.
-  auto finalize = [&](int r) {
-    if (lost_cnt > 0) {
-      double upen = 0.0;
-#pragma unroll
-      for (int sk = 0; sk < K; sk++)
-        upen += c.pen_per_sku ? (double)u[sk] * c.pen[sk] : ((double)u[sk] * c.skw[sk]) * c.pen_scalar;
-      if (c.lost_type == MSC_LOST_CLOSEST) {
-        const int w0 = CLt[r];
-        Lpen[w0 * BS] += upen;
-        if (dbg && info.lost_sales)
-#pragma unroll
-          for (int sk = 0; sk < K; sk++) info.lost_sales[e * WK + w0 * K + sk] += (double)u[sk];
-      } else if (c.lost_type == MSC_LOST_SHIPMENT) {
-        double tot = 0.0;
-        double qr[WM];
-#pragma unroll
-        for (int w = 0; w < WM; w++) {
-          qr[w] = 0.0;
-          if (w < W && (touched >> w & 1u)) {
-            int acc = 0;
-#pragma unroll
-            for (int sk = 0; sk < K; sk++) acc += Lqsr[(w * K + sk) * BS];
-            qr[w] = (double)acc;
-          }
-          tot += qr[w];
-        }
-        if (tot > 0.0) {
-#pragma unroll
-          for (int w = 0; w < WM; w++) {
-            if (qr[w] > 0.0) {
-              const double wt = qr[w] / tot;
-              Lpen[w * BS] += wt * upen;
-              if (dbg && info.lost_sales)
-#pragma unroll
-                for (int sk = 0; sk < K; sk++) info.lost_sales[e * WK + w * K + sk] += wt * (double)u[sk];
-            }
-          }
-        } else {
-          const int w0 = CLt[r];
-          Lpen[w0 * BS] += upen;
-          if (dbg && info.lost_sales)
-#pragma unroll
-            for (int sk = 0; sk < K; sk++) info.lost_sales[e * WK + w0 * K + sk] += (double)u[sk];
-        }
-      } else {  // cost: softmax(-(of * lost_orders + ov * lost_weight) / alpha)
-        double lw = 0.0;
-#pragma unroll
-        for (int sk = 0; sk < K; sk++) lw += (double)u[sk] * c.skw[sk];
-        double lg[WM], mx = -INFINITY, se = 0.0;
-#pragma unroll
-        for (int w = 0; w < WM; w++) {
-          lg[w] = w < W ? -(cof[w] * (double)lost_cnt + cov[w] * lw) / c.alpha : -INFINITY;  // r == cached region
-          mx = lg[w] > mx ? lg[w] : mx;
-        }
-#pragma unroll
-        for (int w = 0; w < WM; w++) {
-          lg[w] = w < W ? exp(lg[w] - mx) : 0.0;
-          se += lg[w];
-        }
-#pragma unroll
-        for (int w = 0; w < WM; w++) {
-          if (w < W) {
-            const double wt = lg[w] / se;
-            Lpen[w * BS] += wt * upen;
-            if (dbg && info.lost_sales)
-#pragma unroll
-              for (int sk = 0; sk < K; sk++) info.lost_sales[e * WK + w * K + sk] += wt * (double)u[sk];
-          }
-        }
-      }
-    }
-    // home-region features: incoming demand and units shipped home (multi_env.py:767-773)
-    unsigned hm = HMt[r];
-    while (hm) {
-      const int w = __builtin_ctz(hm);
-      hm &= hm - 1u;
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) {
-        s.inc[(int64_t)(w * K + sk) * E + e] = dsum[sk];
-        Lshh[(w * K + sk) * BS] = Lqsr[(w * K + sk) * BS];
-      }
-    }
-    if (dbg) {
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) {
-        if (info.demand_per_region) info.demand_per_region[(e * R + r) * K + sk] = dsum[sk];
-        if (info.unfulfilled_demands) info.unfulfilled_demands[(e * R + r) * K + sk] = u[sk];
-      }
-      if (info.lost_order_counts) info.lost_order_counts[e * R + r] = lost_cnt;
-    }
-#pragma unroll
-    for (int w = 0; w < WM; w++)
-      if (w < W && (touched >> w & 1u))
-#pragma unroll
-        for (int sk = 0; sk < K; sk++) Lqsr[(w * K + sk) * BS] = 0;
-  };
-
-  const int maxwh = c.max_wh;
-  // nz[s]: bitmask of warehouses holding stock of SKU s, kept exact through every fill. The
-  // greedy loop only ever ships from a warehouse that has stock of a still-needed SKU, so the
-  // ranked visit of demand_allocator.py:180-203 is equivalent to repeated argmin over that
-  // candidate set (lowest index on cost ties = a stable argsort), and an order whose SKUs are
-  // out of stock everywhere is lost without ranking anything.
-  unsigned nz[K];
-#pragma unroll
-  for (int sk = 0; sk < K; sk++) nz[sk] = 0u;
-  for (int w = 0; w < W; w++)
-#pragma unroll
-    for (int sk = 0; sk < K; sk++) nz[sk] |= Linv[(w * K + sk) * BS] > 0 ? (1u << w) : 0u;
-  if (c.ablate & 2) n_orders = 0;  // timing-only ablation (MSC_ABLATE), never set in production
-  // order records are software-pipelined PF ahead through a register ring (raw uint4 words, so
-  // the loads stay in flight); the loop runs once past the last order as a sentinel so the region
-  // epilogue has a single call site
-  constexpr int NVR = Rec<K>::NV;
-#ifndef MSC_PF
-#define MSC_PF 4
-#endif
-  constexpr int PF = MSC_PF;
-  uint4 ring[PF][NVR];
-#pragma unroll
-  for (int q = 0; q < PF; q++)
-#pragma unroll
-    for (int j = 0; j < NVR; j++) ring[q][j] = (q < n_orders) ? gload4(src, q * rec_step + j * stride) : make_uint4(0, 0, 0, 0);
-  PROF_DECL(sp_loop);
-  PROF_DECL(sp_fin);
-  PROF_DECL(sp_alloc);
-  PROF_DECL(sn_iter);
-  PROF_DECL(sn_fin);
-  PROF_T(ts_loop);
-  for (int oi = 0; oi <= n_orders; oi++) {
-    PROF_ADD(sn_iter, 1);
-    int r = -1;
-    int d[K];
-    {
-      union {
-        uint4 v[NVR];
-        uint16_t h[8 * NVR];
-      } u;
-#pragma unroll
-      for (int j = 0; j < NVR; j++) u.v[j] = ring[0][j];
-      if (oi < n_orders) r = u.h[0];
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) d[sk] = u.h[1 + sk];
-    }
-#pragma unroll
-    for (int q = 0; q + 1 < PF; q++)
-#pragma unroll
-      for (int j = 0; j < NVR; j++) ring[q][j] = ring[q + 1][j];
-    if (oi + PF < n_orders) {
-#pragma unroll
-      for (int j = 0; j < NVR; j++) ring[PF - 1][j] = gload4(src, (oi + PF) * rec_step + j * stride);
-    }
-    if (r != cur) {
-      PROF_T(ts_fin);
-      if (cur >= 0) finalize(cur);
-      PROF_ADD(sp_fin, PROF_NOW() - ts_fin);
-      PROF_ADD(sn_fin, 1);
-      if (r >= 0) load_costs(r);
-      cur = r;
-      lost_cnt = 0;
-      touched = 0;
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
-    }
-    if (oi == n_orders) break;
-    bool any_d = false;
-    double tw = 0.0;
-#pragma unroll
-    for (int sk = 0; sk < K; sk++) {
-      dsum[sk] += d[sk];
-      any_d |= d[sk] > 0;
-      tw += (double)d[sk] * c.skw[sk];
-    }
-    if (!any_d) continue;  // an empty order ships nothing and is never lost
-    int rem[K];
-    unsigned cand = 0u;
-#pragma unroll
-    for (int sk = 0; sk < K; sk++) {
-      rem[sk] = d[sk];
-      cand |= d[sk] > 0 ? nz[sk] : 0u;
-    }
-    PROF_T(ts_alloc);
-    if (cand) {
-      double cst[WM];  // cost = fixed + variable * order weight (demand_allocator.py:168-172)
-#pragma unroll
-      for (int w = 0; w < WM; w++) cst[w] = (w < W && (cand >> w & 1u)) ? cof[w] + cov[w] * tw : INFINITY;
-      int used = 0;
-      while (cand && used < maxwh) {
-        int w = 0;
-        double bc = INFINITY;
-#pragma unroll
-        for (int j = 0; j < WM; j++) {
-          const bool better = (cand >> j & 1u) && cst[j] < bc;
-          bc = better ? cst[j] : bc;
-          w = better ? j : w;
-        }
-        cand &= ~(1u << w);
-        int fl[K];
-        bool any = false;
-#pragma unroll
-        for (int sk = 0; sk < K; sk++) {
-          const int iv = Linv[(w * K + sk) * BS];
-          fl[sk] = rem[sk] < iv ? rem[sk] : iv;
-          any |= fl[sk] > 0;
-        }
-        if (!any) continue;
-        double fw = 0.0;
-        int fsum = 0;
-        bool done = true;
-        unsigned need = 0u;
-#pragma unroll
-        for (int sk = 0; sk < K; sk++) {
-          const int idx = (w * K + sk) * BS;
-          const int left_inv = Linv[idx] - fl[sk];
-          Linv[idx] = left_inv;
-          Lqsr[idx] += fl[sk];
-          Lsht[idx] += fl[sk];
-          nz[sk] &= left_inv > 0 ? ~0u : ~(1u << w);
-          rem[sk] -= fl[sk];
-          done &= rem[sk] <= 0;
-          need |= rem[sk] > 0 ? nz[sk] : 0u;
-          fsum += fl[sk];
-          fw += (double)fl[sk] * c.skw[sk];
-          if (dbg) {
-            if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] += fl[sk];
-            if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
-          }
-        }
-        if (fw == tw) {
-          Lout[w * BS] += bc;  // whole order from w: the ranking cost is of + ov * tw bit for bit
-        } else {
-          double ofw = 0.0, ovw = 0.0;
-#pragma unroll
-          for (int j = 0; j < WM; j++) {
-            ofw = j == w ? cof[j] : ofw;
-            ovw = j == w ? cov[j] : ovw;
-          }
-          Lout[w * BS] += ofw + ovw * fw;
-        }
-        touched |= 1u << w;
-        used++;
-        if (dbg) {
-          if (info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] += 1;
-          if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] += fsum;
-        }
-        if (done) break;
-        cand &= need;  // only warehouses that still hold a needed SKU can contribute
-      }
-    }
-    PROF_ADD(sp_alloc, PROF_NOW() - ts_alloc);
-    bool anyrem = false;
-#pragma unroll
-    for (int sk = 0; sk < K; sk++) {
-      anyrem |= rem[sk] > 0;
-      u[sk] += rem[sk] > 0 ? rem[sk] : 0;
-    }
-    lost_cnt += anyrem ? 1 : 0;
-  }
-  PROF_ADD(sp_loop, PROF_NOW() - ts_loop);
-  PROF_FLUSH(10, sp_loop);
-  PROF_FLUSH(11, sp_fin);
-  PROF_FLUSH(12, sp_alloc);
-  PROF_FLUSH(13, sn_iter);
-  PROF_FLUSH(14, sn_fin);
-  PROF_FLUSH(15, 1ull);
-
-  // ---- phase C: inventory, history, forecast, rewards, observations -------------------------
-  const int hslot = t % MSC_HISTORY;
-  for (int i = 0; i < WK; i++) {
-    s.inv[i * E + e] = Linv[i * BS];
-    const int v = s.inc[i * E + e];
-    s.hist[((int64_t)hslot * WK + i) * E + e] = v;
-    // EMA forecast in float32: 0.3 * x + 0.7 * f (python floats are weak scalars under NEP 50)
-    s.fc[i * E + e] = 0.3f * (float)v + 0.7f * s.fc[i * E + e];
-  }
-  double rw[WM];
-  double team = 0.0;
-#pragma unroll
-  for (int w = 0; w < WM; w++) {
-    rw[w] = 0.0;
-    if (w < W) {
-      double hold = 0.0;
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) {
-        const double iv = (double)Linv[(w * K + sk) * BS];
-        hold += c.hold_per_sku ? iv * c.hold[sk] : (iv * c.skw[sk]) * c.hold_scalar;
-      }
-      const double pen = Lpen[w * BS], out = Lout[w * BS], inb = Linb[w * BS];
-      rw[w] = -((((hold + pen) + out) + inb) * c.scale);
-      team += rw[w];
-      if (dbg && info.costs) {
-        info.costs[(e * 4 + 0) * W + w] = hold;
-        info.costs[(e * 4 + 1) * W + w] = pen;
-        info.costs[(e * 4 + 2) * W + w] = out;
-        info.costs[(e * 4 + 3) * W + w] = inb;
-      }
-    }
-  }
-#pragma unroll
-  for (int w = 0; w < WM; w++) {
-    if (w < W) {
-      const double v = c.scope == MSC_SCOPE_TEAM ? team : rw[w];
-      io.rew[e * W + w] = (float)v;
-      if (io.rew64) io.rew64[e * W + w] = v;
-    }
-  }
-  const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
-  const bool trunc = t + 1 >= c.T;
-  io.trunc[e] = trunc ? 1 : 0;
-  const int64_t obs_off = e * W * c.L;
-  if (!trunc) {
-    s.t[e] = t + 1;
-    if (!(c.ablate & 1)) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, io.obs + obs_off);
-  } else {
-    if (io.final_obs) build_obs<K>(c, s, e, t, n_hist, Lshh, Lsht, io.final_obs + obs_off);
-    reset_env<K>(c, s, e, 0, nullptr);
-    build_obs<K>(c, s, e, 0, 0, nullptr, nullptr, io.obs + obs_off);
-  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2502,7 +1458,7 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __
     const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
     trunc = t + 1 >= c.T;
     if (!trunc) {
-      if (!(c.ablate & 1)) build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.obs + obs_off);
+      build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.obs + obs_off);
     } else if (io.final_obs) {
       build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
     }
@@ -2538,8 +1494,6 @@ __global__ void obs_flat_kernel(const float* __restrict__ obs, float* __restrict
 // ------------------------------------------------------------------------------------------
 int order_record_vec4(int K) { return (1 + K + 7) / 8; }
 
-size_t step_lds_bytes(const EnvConst& c) { return step_lds_bytes_for(c, c.cost_lds != 0); }
-
 #define MSC_K_SWITCH(KV, BODY) \
   switch (KV) {                \
     case 1: { constexpr int K = 1; BODY; } break; \
@@ -2561,9 +1515,7 @@ hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask,
   return hipGetLastError();
 }
 
-static size_t park_fixed(const EnvConst& c) {
-  return c.demand_impl == 4 ? park_lds_fixed() : c.demand_impl == 5 ? park4_lds_fixed() : unit_lds_fixed();
-}
+static size_t park_fixed(const EnvConst& c) { return c.demand_impl == 5 ? park4_lds_fixed() : unit_lds_fixed(); }
 static bool park_lds_tables(const EnvConst& c) {
   return park_fixed(c) + (size_t)(2 + c.K) * c.R * sizeof(double) <= 40 * 1024;
 }
@@ -2577,9 +1529,7 @@ static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t 
   const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
   const bool t = park_lds_tables(c);
   DFn fn;
-  if (c.demand_impl == 4)  // single-draw hot steps (A/B: MSC_DEMAND_IMPL=park1)
-    fn = t ? (DFn)demand_park_kernel<K, G, true> : (DFn)demand_park_kernel<K, G, false>;
-  else if (c.demand_impl == 5)  // 4-draw parking parser (A/B: MSC_DEMAND_IMPL=park4)
+  if (c.demand_impl == 5)  // 4-draw parking parser (A/B: MSC_DEMAND_IMPL=park4)
     fn = t ? (DFn)demand_park4_kernel<K, G, true> : (DFn)demand_park4_kernel<K, G, false>;
   else
     fn = t ? (DFn)demand_unit_kernel<K, G, true> : (DFn)demand_unit_kernel<K, G, false>;
@@ -2588,27 +1538,12 @@ static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t 
 
 template <int K>
 static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st) {
-  const size_t lds = c.dem_lds ? (size_t)(2 + K) * c.R * sizeof(double) : 0;
-  if (c.demand_impl == 1)
-    hipLaunchKernelGGL(demand_poisson_nested_kernel<K>, grid_for(c.E), dim3(BS), 0, st, d);
-  else if (c.demand_impl == 2)
-    hipLaunchKernelGGL(demand_poisson_kernel<K>, grid_for(c.E), dim3(BS), lds, st, d);
-  else if (c.demand_impl == 3) {
-    if (c.dem_lds)
-      hipLaunchKernelGGL((demand_flat_kernel<K, true>), grid_for(c.E, c.epw_dem), dim3(BS), lds, st, d);
-    else
-      hipLaunchKernelGGL((demand_flat_kernel<K, false>), grid_for(c.E, c.epw_dem), dim3(BS), 0, st, d);
-  } else if (c.demand_gen == 1) {
+  if (c.demand_gen == 1)
     launch_split_demand<K, 1>(c, d, st);
-  } else if (c.demand_gen == 3) {
-    launch_split_demand<K, 3>(c, d, st);
-  } else if (c.demand_gen == 4) {
-    launch_split_demand<K, 4>(c, d, st);
-  } else if (c.demand_gen == 7) {
-    launch_split_demand<K, 7>(c, d, st);
-  } else {
+  else if (c.demand_gen == 2)
     launch_split_demand<K, 2>(c, d, st);
-  }
+  else
+    launch_split_demand<K, 3>(c, d, st);
 }
 
 hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st) {
@@ -2618,33 +1553,24 @@ hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st) {
 
 template <int K>
 static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen, hipStream_t st) {
-  const size_t lds = step_lds_bytes(c);
   if (gen && c.demand_type == MSC_DEMAND_POISSON) launch_demand_k<K>(c, d, st);
   using KFn = void (*)(const DevEnv*, StepIO);
-  if (c.step_impl == 0) {  // production: three phase kernels, group-per-env allocation
-    const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : c.W <= 8 ? 8 : 16;
-    const bool dbg = io.has_info != 0;  // collect_step_info: the instrumented instantiations
-    KFn a = dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>;
-    KFn cc = dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>;
-    const bool tab = step_b_tab_bytes(c.R, c.W) <= STEP_B_TAB_MAX;
-    KFn b;
+  // three phase kernels, group-per-env allocation
+  const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : c.W <= 8 ? 8 : 16;
+  const bool dbg = io.has_info != 0;  // collect_step_info: the instrumented instantiations
+  KFn a = dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>;
+  KFn cc = dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>;
+  const bool tab = step_b_tab_bytes(c.R, c.W) <= STEP_B_TAB_MAX;
+  KFn b;
 #define MSC_SB(GWV)                                                                                   \
   (dbg ? (tab ? (KFn)step_b_kernel<K, GWV, true, true> : (KFn)step_b_kernel<K, GWV, true, false>)   \
        : (tab ? (KFn)step_b_kernel<K, GWV, false, true> : (KFn)step_b_kernel<K, GWV, false, false>))
-    b = GW == 2 ? MSC_SB(2) : GW == 4 ? MSC_SB(4) : GW == 8 ? MSC_SB(8) : MSC_SB(16);
+  b = GW == 2 ? MSC_SB(2) : GW == 4 ? MSC_SB(4) : GW == 8 ? MSC_SB(8) : MSC_SB(16);
 #undef MSC_SB
-    const size_t lds_a = c.lead_type == MSC_LEAD_STOCHASTIC ? (size_t)c.W * K * BS * sizeof(int32_t) : 0;
-    hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * c.W), lds_a, st, d, io);
-    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
-    hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), (size_t)c.W * BS * sizeof(double), st, d, io);
-    return hipGetLastError();
-  }
-  const bool t = c.cost_lds != 0;
-  KFn fn;
-  if (c.W <= 4) fn = t ? (KFn)step_kernel<K, 4, true> : (KFn)step_kernel<K, 4, false>;
-  else if (c.W <= 8) fn = t ? (KFn)step_kernel<K, 8, true> : (KFn)step_kernel<K, 8, false>;
-  else fn = t ? (KFn)step_kernel<K, 16, true> : (KFn)step_kernel<K, 16, false>;
-  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_step), dim3(BS), lds, st, d, io);
+  const size_t lds_a = c.lead_type == MSC_LEAD_STOCHASTIC ? (size_t)c.W * K * BS * sizeof(int32_t) : 0;
+  hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * c.W), lds_a, st, d, io);
+  hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
+  hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), (size_t)c.W * BS * sizeof(double), st, d, io);
   return hipGetLastError();
 }
 
