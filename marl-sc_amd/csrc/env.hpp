@@ -32,6 +32,7 @@ struct EnvConst {
   int32_t demand_gen;   // generator waves per block of the split demand kernel (1, 2 or 3)
   int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
   int32_t parser_rot;   // which wave of a demand block parses: (wave + rot(block)) % (1 + G) == 0 (A/B knob)
+  int32_t obs_stage;    // 1: step_c stages each wave's observations in LDS and writes them coalesced
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
   uint32_t flags;
   int64_t E;

@@ -1444,6 +1444,12 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __
   __syncthreads();
   bool trunc = false;
   const int64_t obs_off = e * W * c.L;
+  // observation staging: this wave's 64 agents' vectors [lane][L + 1] (odd stride), written to
+  // HBM afterwards as runs of consecutive floats (a lane's own vector is L floats at a stride of
+  // W*L floats from the next env's: storing it directly leaves 64 partially written lines per
+  // store instruction, ~5x the algorithmic write bytes in the PMC counters)
+  const int L = c.L;
+  float* stg = reinterpret_cast<float*>(Lrw + W * BS) + (int64_t)wave * BS * (L + 1);
   // shipped home / total of this step, [(w*K+s) * E] from the env's column
   const int32_t* shh = s.sc_shh + e;
   const int32_t* sht = s.sc_sht + e;
@@ -1458,9 +1464,28 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __
     const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
     trunc = t + 1 >= c.T;
     if (!trunc) {
-      build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.obs + obs_off);
+      build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E,
+                         c.obs_stage ? stg + lane * (L + 1) - (int64_t)w * L : io.obs + obs_off);
     } else if (io.final_obs) {
       build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
+    }
+  }
+  if (c.obs_stage && wave < W) {
+    // copy-out: flat index i = env * L + j over the wave's 64 vectors, 64 consecutive i per store
+    const uint64_t skip = __ballot(!act || trunc);  // envs whose vector is not in the stage
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int q = BS / L, rr = BS % L;
+    int ev = lane / L, j = lane % L;
+    const int64_t e0 = (int64_t)blockIdx.x * BS;
+    for (int it = 0; it < L; it++) {
+      if (!((skip >> ev) & 1ull)) io.obs[((e0 + ev) * W + w) * L + j] = stg[ev * (L + 1) + j];
+      j += rr;
+      ev += q;
+      if (j >= L) {
+        j -= L;
+        ev += 1;
+      }
     }
   }
   // truncation: reset the env (one sequential RNG pass per env), then every agent's reset obs
@@ -1570,7 +1595,8 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
   const size_t lds_a = c.lead_type == MSC_LEAD_STOCHASTIC ? (size_t)c.W * K * BS * sizeof(int32_t) : 0;
   hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * c.W), lds_a, st, d, io);
   hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
-  hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), (size_t)c.W * BS * sizeof(double), st, d, io);
+  const size_t lds_c = (size_t)c.W * BS * sizeof(double) + (c.obs_stage ? (size_t)c.W * BS * (c.L + 1) * sizeof(float) : 0);
+  hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), lds_c, st, d, io);
   return hipGetLastError();
 }
 
