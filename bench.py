@@ -252,7 +252,7 @@ def main():
                 "ms_per_step": round(t_roll / args.rollout_T * 1e3, 4), "T": args.rollout_T,
                 "policy": f"MAPPO (config_files/algorithms/mappo.yaml): actor {spec.local_obs_dim}-256-256-{spec.K}, "
                           f"critic {spec.local_obs_dim * (1 + spec.W)}-64-64-1, fp32, parameter sharing",
-                "includes": "env step, obs_flat for the critic, actor+critic forward, Gaussian sampling, "
+                "includes": "env step, actor forward, MAPPO critic on local||global (first layer split: global block once per env), Gaussian sampling, "
                             "buffer writes, truncation bootstrap, GAE kernel, adv-norm all-reduce + normalise"}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)

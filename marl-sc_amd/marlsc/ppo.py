@@ -36,7 +36,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from .rollout import MLP, RolloutCollector, RolloutConfig
+from .rollout import MLP, RolloutCollector, RolloutConfig, split_global_mlp
 
 LOG2PI = math.log(2 * math.pi)
 ENTROPY_CONST = 0.5 * math.log(2 * math.pi * math.e)
@@ -176,6 +176,11 @@ class MultiAgentActorCritic(nn.Module):
         return mean, log_std
 
     def values(self, local_obs, full_obs=None):
+        if self.rc.critic_obs_type == "global" and full_obs is None:  # split first layer (rollout.py)
+            if self.shared:
+                return split_global_mlp(self.policies[0].critic, local_obs).squeeze(-1)
+            return torch.stack([split_global_mlp(p.critic, local_obs, w).squeeze(-1)
+                                for w, p in enumerate(self.policies)], dim=-1)
         x = self._x(local_obs, full_obs, self.rc.critic_obs_type)
         if self.shared:
             return self.policies[0].critic(x).squeeze(-1)
@@ -411,7 +416,7 @@ class PPOTrainer:
         self._completed: List[float] = []
 
     def _full_fn(self):
-        if "global" not in (self.cfg.actor_obs_type, self.cfg.critic_obs_type):
+        if self.cfg.actor_obs_type != "global":  # the critic evaluates its split first layer
             return None
         W, L = self.env.W, self.env.local_obs_dim
 

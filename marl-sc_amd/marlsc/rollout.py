@@ -97,8 +97,29 @@ class ActorCritic(nn.Module):
         return mean, log_std
 
     def values(self, local_obs: torch.Tensor, full_obs: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if self.rc.critic_obs_type == "global" and full_obs is None:
+            return split_global_mlp(self.critic, local_obs).squeeze(-1)
         x = full_obs if self.rc.critic_obs_type == "global" else local_obs
         return self.critic(x).squeeze(-1)
+
+
+def split_global_mlp(mlp: nn.Sequential, local_obs: torch.Tensor, agent: Optional[int] = None) -> torch.Tensor:
+    """An MLP over the per-agent flat input local_w || (local_0 .. local_{W-1}) evaluated from the
+    local observations [..., W, L] without materialising it: the first Linear's columns split into
+    a local block (per agent) and a global block (once per env, shared by its W agents) --
+    mathematically the same layer, ~W x fewer first-layer flops and no [E, W, L(1+W)] buffer.
+    agent=None: all W agents ([..., W, out]); agent=w: agent w only ([..., out])."""
+    first = mlp[0]
+    W, L = local_obs.shape[-2], local_obs.shape[-1]
+    glob = local_obs.reshape(*local_obs.shape[:-2], W * L)
+    g = torch.nn.functional.linear(glob, first.weight[:, L:])
+    if agent is None:
+        h = torch.nn.functional.linear(local_obs, first.weight[:, :L], first.bias) + g.unsqueeze(-2)
+    else:
+        h = torch.nn.functional.linear(local_obs[..., agent, :], first.weight[:, :L], first.bias) + g
+    for layer in list(mlp)[1:]:
+        h = layer(h)
+    return h
 
 
 def _vp(t: Optional[torch.Tensor]):
@@ -152,7 +173,7 @@ class RolloutCollector:
         self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
         self._flat = torch.empty((E, W, L * (1 + W)), device=dev)
         self._gen = torch.Generator(device=dev).manual_seed(seed)
-        self._need_flat = "global" in (module.rc.actor_obs_type, module.rc.critic_obs_type)
+        self._need_flat = module.rc.actor_obs_type == "global"  # the critic splits its first layer
 
     def _full(self, obs):
         return self.env.obs_flat(obs=obs, out=self._flat) if self._need_flat else None
@@ -170,13 +191,18 @@ class RolloutCollector:
             a = mean + std * torch.randn(mean.shape, device=mean.device, generator=self._gen)
             self.actions[t] = a
             self.logp[t] = (-((a - mean) ** 2) / (2 * std * std) - log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+            may_end = env.may_truncate()
             obs, rew, trunc, final_obs = env.step(a.clamp_(-1.0, 1.0))
             self.rewards[t] = rew
             self.truncated[t] = trunc.unsqueeze(-1)
             # truncation bootstrap: V(final_obs) for the envs whose episode ended at this step
-            full_f = self._full(final_obs)
-            self.next_values[t] = torch.where(trunc.bool().unsqueeze(-1), m.values(final_obs, full_f),
-                                              torch.zeros((), device=obs.device))
+            # (skipped while the envs are known to be mid-episode in lockstep)
+            if may_end:
+                full_f = self._full(final_obs)
+                self.next_values[t] = torch.where(trunc.bool().unsqueeze(-1), m.values(final_obs, full_f),
+                                                  torch.zeros((), device=obs.device))
+            else:
+                self.next_values[t].zero_()
         self.values[T] = m.values(obs, self._full(obs))
         N = self.N
         gae(self.rewards.view(T, N), self.values.view(T + 1, N), self.next_values.view(T, N),

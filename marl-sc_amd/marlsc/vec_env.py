@@ -93,6 +93,7 @@ class VecInventoryEnv:
         s = None if root_seeds is None else root_seeds.to(device=self.device, dtype=torch.int64).to(torch.int32).contiguous()
         flags = abi.RESET_EVAL_RESTART if eval_restart else 0
         abi.check(abi.lib().msc_env_reset(self._h, _p(m), _p(s), flags, _p(self.obs), _stream()))
+        self._t_sync = 0 if mask is None else -1  # common timestep of every env (-1: unknown)
         return self.obs
 
     def step(self, actions: torch.Tensor, *, want_final_obs: bool = True, want_f64: bool = False,
@@ -113,7 +114,15 @@ class VecInventoryEnv:
         abi.check(abi.lib().msc_env_step(
             self._h, _p(actions), _p(self.obs), _p(self.rewards), _p(self.rewards_f64) if want_f64 else None,
             _p(self.truncated), _p(self.final_obs) if want_final_obs else None, si, _stream()))
+        ts = getattr(self, "_t_sync", -1)
+        self._t_sync = -1 if ts < 0 else (0 if ts + 1 >= self.spec.episode_length else ts + 1)
         return self.obs, self.rewards, self.truncated, (self.final_obs if want_final_obs else None)
+
+    def may_truncate(self) -> bool:
+        """Whether the next step() can end an episode (host-side lockstep tracking, no sync): False
+        only while every env is known to sit at the same timestep before the last one."""
+        ts = getattr(self, "_t_sync", -1)
+        return ts < 0 or ts + 1 >= self.spec.episode_length
 
     def generate_demand(self) -> None:
         """Draw the next step's demand now (see msc_env_generate_demand); overlappable."""
@@ -158,6 +167,7 @@ class VecInventoryEnv:
         return bytes(buf)
 
     def load_state(self, blob: bytes) -> None:
+        self._t_sync = -1
         n = abi.lib().msc_env_state_bytes(self._h)
         if len(blob) != n:
             raise ValueError(f"state blob has {len(blob)} bytes, expected {n}")

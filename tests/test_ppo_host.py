@@ -206,3 +206,17 @@ def test_cli_accepts_the_reference_arguments_and_script_is_executable():
     sh = REPO / "scripts" / "run_experiment.sh"
     assert os.access(sh, os.X_OK)
     assert subprocess.run(["bash", "-n", str(sh)]).returncode == 0
+
+
+def test_split_first_layer_critic_equals_the_flat_input_critic():
+    # the critic over local_w || (local_0..local_{W-1}) evaluated from the local observations only
+    from marlsc.ppo import MultiAgentActorCritic
+    cfg = _cfg("mappo")
+    rc = cfg.rollout_config()
+    W, L, K = 4, 9, 3
+    for shared in (True, False):
+        torch.manual_seed(3)
+        m = MultiAgentActorCritic(W, L, L * W, K, rc, shared).double()
+        obs = torch.randn(6, W, L, dtype=torch.float64)
+        full = torch.cat([obs, obs.reshape(6, 1, W * L).expand(6, W, W * L)], -1)
+        torch.testing.assert_close(m.values(obs), m.values(obs, full), rtol=1e-12, atol=1e-12)
