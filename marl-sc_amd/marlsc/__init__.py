@@ -13,7 +13,7 @@ from .synthetic import make_synthetic_env_config
 __all__ = [
     "ConfigNode", "load_environment_config", "load_feature_config", "validate_environment_config",
     "SeedManager", "default_train_seed", "EnvSpec", "make_synthetic_env_config",
-    "VecInventoryEnv", "InventoryEnvironment",
+    "VecInventoryEnv", "InventoryEnvironment", "CentralizedEnvWrapper", "VecCentralizedEnv",
 ]
 
 
@@ -24,4 +24,7 @@ def __getattr__(name):  # torch-dependent modules load lazily
     if name == "InventoryEnvironment":
         from .env import InventoryEnvironment
         return InventoryEnvironment
+    if name in ("CentralizedEnvWrapper", "VecCentralizedEnv"):
+        from . import single_env
+        return getattr(single_env, name)
     raise AttributeError(name)
