@@ -643,6 +643,12 @@ __host__ __device__ constexpr size_t unit_lds_fixed() {
   return (size_t)BS * USLOTS * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
 }
 
+#ifndef MSC_PARSER_PRIO
+#define MSC_PARSER_PRIO 2  // s_setprio of the parser wave (generators: MSC_GEN_PRIO)
+#endif
+#ifndef MSC_GEN_PRIO
+#define MSC_GEN_PRIO 1
+#endif
 #ifndef MSC_DEM_WPE
 #define MSC_DEM_WPE 8  // <= 64 VGPRs: two demand waves fit beside four step_b waves on a SIMD
 #endif
@@ -683,6 +689,7 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
 
   if (wave > 0) {
     // ---------------- generator g: stream positions g, g + G, g + 2G, ...
+    if (MSC_GEN_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_GEN_PRIO);
     const int g = wave - 1;
     uint64_t th = 0, tl = 0, ih = 0, il = 1;
     if (valid) {
@@ -724,7 +731,7 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   // Older and higher-priority waves win VALU issue arbitration on a SIMD (MI355X_MICROARCH.md,
   // wave scheduling): the parser is the per-env critical path, the generators only need to stay
   // a chunk ahead of it.
-  __builtin_amdgcn_s_setprio(2);
+  __builtin_amdgcn_s_setprio(MSC_PARSER_PRIO);
   Pcg64 r0{};
   if (valid) {
     r0 = load_rng(s, 0, e, E);
@@ -1056,6 +1063,12 @@ __device__ __forceinline__ double group_np_sum(double v, int n) {
 
 // step_b waves per SIMD the register budget is sized for: 5 (<= 96 VGPRs) leaves room on each SIMD
 // for a demand-kernel wave of the next step next to the four step_b waves of this one
+#ifndef MSC_SC_PRIO
+#define MSC_SC_PRIO 0  // s_setprio of the step_c waves
+#endif
+#ifndef MSC_SB_PRIO
+#define MSC_SB_PRIO 3  // s_setprio of the step_b waves (above the next step's demand waves)
+#endif
 #ifndef MSC_SB_WPE
 #define MSC_SB_WPE 5
 #endif
@@ -1085,6 +1098,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
   static_assert(CH >= 1 && SB_REC % 64 == 0, "window layout");
   extern __shared__ __attribute__((aligned(16))) uint4 sb_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, gbase = lane & ~(GW - 1);
+  if (MSC_SB_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SB_PRIO);
   uint4* win = sb_lds + wave * 2 * SB_REC;  // this wave's two windows [2][CH][NVR][EPW]
   const MSC_GLOBAL int32_t* closest = gp(c.closest);
   double* lof = TAB ? reinterpret_cast<double*>(sb_lds + 4 * 2 * SB_REC) : nullptr;
@@ -1411,6 +1425,7 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __
   const int W = c.W, WK = W * K;
   const int64_t E = c.E;
   const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;
+  if (MSC_SC_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SC_PRIO);
   const int64_t e = (int64_t)blockIdx.x * BS + lane;
   const bool act = wave < W && e < E;
   const int w = wave;
