@@ -150,25 +150,17 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     env.check()
-    # (2) per-kernel device durations for the roofline: the same kernels issued one at a time on
-    #     torch's current stream (explicit msc_env_generate_demand, then msc_env_step) and
-    #     bracketed with HIP events on that stream
+    # (2) per-launch device durations for the roofline, in the production (pipelined) regime:
+    #     the library brackets each demand launch and each step launch (step_a/b/c) with HIP events
+    #     on the stream it runs on (side stream for pipelined demand), msc_env_set_timing
     KP = min(K, 50)
-    env.set_pipelining(False)
-    env.step(pool[0])  # consumes the demand already generated ahead by the pipelined run
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(KP)]
-    torch.cuda.synchronize()
+    env.set_timing(KP)
     for i in range(KP):
-        e0, e1, e2 = evs[i]
-        e0.record()
-        env.generate_demand()
-        e1.record()
         env.step(pool[i % 8])
-        e2.record()
-    torch.cuda.synchronize()
+    tm = env.read_timing()
+    env.set_timing(0)
     env.check()
-    t_demand = sum(a.elapsed_time(b) for a, b, _ in evs) / KP / 1e3
-    t_step = sum(b.elapsed_time(c) for _, b, c in evs) / KP / 1e3
+    t_demand, t_step = tm["demand_ms"] / 1e3, tm["step_ms"] / 1e3
     # (3) MAPPO rollout (configs[2]): env step + actor/critic forward + sampling + buffer writes +
     #     GAE kernel + adv-norm statistics all-reduce, T steps per rollout
     t_roll = 0.0

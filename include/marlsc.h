@@ -195,6 +195,17 @@ int msc_env_generate_demand(msc_env* env, msc_stream_t stream);
  * way; 0 disables it (every step then runs demand + step back to back on the caller's stream). */
 int msc_env_set_pipelining(msc_env* env, int32_t enabled);
 
+/* Per-launch device durations of the production path (for roofline accounting): with max_steps > 0
+ * the next max_steps calls of msc_env_step bracket their demand launch and their step launch (the
+ * step kernels of that call) with HIP events on the stream each runs on -- the caller's stream, or
+ * the side stream for pipelined demand. 0 disables and frees the events. No reference
+ * counterpart (instrumentation only). */
+int msc_env_set_timing(msc_env* env, int32_t max_steps);
+/* Mean device duration in ms of the recorded demand / step launches and their counts (waits for
+ * the recorded events). */
+int msc_env_read_timing(msc_env* env, double* demand_ms, double* step_ms, int64_t* n_demand,
+                        int64_t* n_step);
+
 /* Flat per-agent observation of the reference [E][W][L*(1+W)] = local_w || local_0..local_{W-1},
  * from the compact obs [E][W][L]. */
 int msc_env_obs_flat(const msc_env* env, const float* obs, float* flat, msc_stream_t stream);

@@ -56,7 +56,22 @@ struct msc_env {
   int t_sync = -1;                 // common timestep of every env, -1 if unknown
   bool ready[2] = {false, false};  // order buffer b holds the demand of the next step using it
   bool pipeline = true;
+  // msc_env_set_timing: event pairs around demand / step launches (2 per launch)
+  std::vector<hipEvent_t> tev_dem, tev_step;
+  int t_cap = 0, n_tdem = 0, n_tstep = 0;
 };
+
+static void timing_free(msc_env* env) {
+  for (hipEvent_t e : env->tev_dem) (void)hipEventDestroy(e);
+  for (hipEvent_t e : env->tev_step) (void)hipEventDestroy(e);
+  env->tev_dem.clear();
+  env->tev_step.clear();
+  env->t_cap = env->n_tdem = env->n_tstep = 0;
+}
+// record event `i` (0 = before, 1 = after) of launch n of `v` on `st`, if timing is on
+static hipError_t tmark(const msc_env* env, const std::vector<hipEvent_t>& v, int n, int i, hipStream_t st) {
+  return n < env->t_cap ? hipEventRecord(v[2 * n + i], st) : hipSuccess;
+}
 
 extern "C" {
 
@@ -430,6 +445,7 @@ void msc_env_destroy(msc_env* env) {
     if (env->ev_step[b]) (void)hipEventDestroy(env->ev_step[b]);
   }
   if (env->ev_reset) (void)hipEventDestroy(env->ev_reset);
+  timing_free(env);
   if (env->side) (void)hipStreamDestroy(env->side);
   delete env;
 }
@@ -504,11 +520,15 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
     if (env->ready[b]) {
       HIP_TRY(hipStreamWaitEvent(st, env->ev_dem[b], 0));
     } else {
+      HIP_TRY(tmark(env, env->tev_dem, env->n_tdem, 0, st));
       HIP_TRY(launch_demand(c, env->dev + b, st));
+      HIP_TRY(tmark(env, env->tev_dem, env->n_tdem++, 1, st));
       HIP_TRY(hipEventRecord(env->ev_dem[b], st));
     }
   }
+  HIP_TRY(tmark(env, env->tev_step, env->n_tstep, 0, st));
   HIP_TRY(launch_step(c, env->dev + b, io, false, st));
+  HIP_TRY(tmark(env, env->tev_step, env->n_tstep++, 1, st));
   HIP_TRY(hipEventRecord(env->ev_step[b], st));
   env->ready[b] = false;
   const bool boundary = env->t_sync < 0 || env->t_sync + 1 >= c.T;
@@ -519,7 +539,9 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
     HIP_TRY(hipStreamWaitEvent(env->side, env->ev_step[nb], 0));
     HIP_TRY(hipStreamWaitEvent(env->side, env->ev_dem[b], 0));
     HIP_TRY(hipStreamWaitEvent(env->side, env->ev_reset, 0));
+    HIP_TRY(tmark(env, env->tev_dem, env->n_tdem, 0, env->side));
     HIP_TRY(launch_demand(c, env->dev + nb, env->side));
+    HIP_TRY(tmark(env, env->tev_dem, env->n_tdem++, 1, env->side));
     HIP_TRY(hipEventRecord(env->ev_dem[nb], env->side));
     env->ready[nb] = true;
   }
@@ -531,6 +553,46 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
 int msc_env_set_pipelining(msc_env* env, int32_t enabled) {
   if (!env) return set_err(-1, "null env");
   env->pipeline = enabled != 0 && env->c.demand_type == MSC_DEMAND_POISSON;
+  return 0;
+}
+
+int msc_env_set_timing(msc_env* env, int32_t max_steps) {
+  if (!env) return set_err(-1, "null env");
+  if (max_steps < 0) return set_err(-1, "max_steps < 0");
+  HIP_TRY(hipSetDevice(env->device));
+  HIP_TRY(hipDeviceSynchronize());
+  timing_free(env);
+  for (int i = 0; i < 2 * max_steps; i++) {
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    env->tev_dem.push_back(a);
+    env->tev_step.push_back(b);
+  }
+  env->t_cap = max_steps;
+  return 0;
+}
+
+int msc_env_read_timing(msc_env* env, double* demand_ms, double* step_ms, int64_t* n_demand, int64_t* n_step) {
+  if (!env) return set_err(-1, "null env");
+  auto mean = [&](const std::vector<hipEvent_t>& v, int n, double* out) -> hipError_t {
+    n = n < env->t_cap ? n : env->t_cap;
+    double sum = 0.0;
+    for (int i = 0; i < n; i++) {
+      hipError_t e = hipEventSynchronize(v[2 * i + 1]);
+      if (e != hipSuccess) return e;
+      float ms = 0.f;
+      e = hipEventElapsedTime(&ms, v[2 * i], v[2 * i + 1]);
+      if (e != hipSuccess) return e;
+      sum += ms;
+    }
+    if (out) *out = n ? sum / n : 0.0;
+    return hipSuccess;
+  };
+  HIP_TRY(mean(env->tev_dem, env->n_tdem, demand_ms));
+  HIP_TRY(mean(env->tev_step, env->n_tstep, step_ms));
+  if (n_demand) *n_demand = env->n_tdem < env->t_cap ? env->n_tdem : env->t_cap;
+  if (n_step) *n_step = env->n_tstep < env->t_cap ? env->n_tstep : env->t_cap;
   return 0;
 }
 

@@ -97,6 +97,9 @@ def lib() -> C.CDLL:
     L.msc_env_obs_flat.argtypes = [vp, vp, vp, vp]
     L.msc_env_generate_demand.argtypes = [vp, vp]
     L.msc_env_set_pipelining.argtypes = [vp, C.c_int32]
+    L.msc_env_set_timing.argtypes = [vp, C.c_int32]
+    L.msc_env_read_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                      C.POINTER(C.c_int64)]
     L.msc_env_read_state.argtypes = [vp, vp, vp, vp, vp]
     L.msc_env_state_bytes.argtypes = [vp]
     L.msc_env_state_bytes.restype = C.c_int64
@@ -122,7 +125,7 @@ def check(rc: int) -> None:
 
 
 EXPORTED_SYMBOLS = [
-    "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_obs_flat",
+    "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_timing", "msc_env_read_timing", "msc_env_obs_flat",
     "msc_env_read_state", "msc_env_state_bytes", "msc_env_save_state", "msc_env_load_state", "msc_env_check",
     "msc_gae", "msc_adv_normalize", "msc_seedseq_u32", "msc_last_error", "msc_abi_version",
 ]

@@ -132,6 +132,18 @@ class VecInventoryEnv:
         """Toggle the library's automatic next-step demand pipelining (results are identical)."""
         abi.check(abi.lib().msc_env_set_pipelining(self._h, int(bool(enabled))))
 
+    def set_timing(self, max_steps: int) -> None:
+        """Bracket the demand / step launches of the next max_steps steps with HIP events on the
+        streams they run on (msc_env_set_timing); 0 turns it off."""
+        abi.check(abi.lib().msc_env_set_timing(self._h, int(max_steps)))
+
+    def read_timing(self) -> Dict[str, float]:
+        """Mean device ms of the timed demand / step launches (msc_env_read_timing)."""
+        import ctypes as C
+        d, s, nd, ns = C.c_double(), C.c_double(), C.c_int64(), C.c_int64()
+        abi.check(abi.lib().msc_env_read_timing(self._h, C.byref(d), C.byref(s), C.byref(nd), C.byref(ns)))
+        return {"demand_ms": d.value, "step_ms": s.value, "n_demand": nd.value, "n_step": ns.value}
+
     def alloc_info(self) -> Dict[str, torch.Tensor]:
         """Device buffers for msc_step_info (the reference's collect_step_info dict)."""
         E, W, K, R = self.n_envs, self.W, self.K, self.R

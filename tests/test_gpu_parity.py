@@ -269,3 +269,23 @@ def test_pipelined_equals_sequential_across_resets_and_checkpoints():
     sa, sb = a.read_state(), b.read_state()
     assert np.array_equal(sa["rng"], sb["rng"])  # reported as of before the demand generated ahead
     assert np.array_equal(sa["inventory"], sb["inventory"])
+
+
+def test_launch_timing_counts_and_results_unchanged():
+    # msc_env_set_timing (bench.py's roofline durations) only adds events: same results, one
+    # demand + one step launch timed per step while enabled, nothing after max_steps
+    cfg = make_synthetic_env_config(4, 8, 3, episode_length=5)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    a, b = _vec(spec, 128, base_seed=3), _vec(spec, 128, base_seed=3)
+    a.reset(), b.reset()
+    a.set_timing(6)
+    rng = np.random.default_rng(4)
+    for t in range(9):
+        act = torch.from_numpy(rng.uniform(-1, 1, (128, 4, 3)).astype(np.float32)).cuda()
+        assert torch.equal(a.step(act)[0], b.step(act)[0]), f"step {t}"
+        assert torch.equal(a.rewards, b.rewards)
+    tm = a.read_timing()
+    assert tm["n_step"] == 6 and tm["n_demand"] == 6
+    assert tm["step_ms"] > 0 and tm["demand_ms"] > 0
+    a.set_timing(0)
+    assert a.read_timing()["n_step"] == 0
