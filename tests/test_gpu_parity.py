@@ -289,3 +289,17 @@ def test_launch_timing_counts_and_results_unchanged():
     assert tm["step_ms"] > 0 and tm["demand_ms"] > 0
     a.set_timing(0)
     assert a.read_timing()["n_step"] == 0
+
+
+@pytest.mark.parametrize("W,R,K,lo,p,lq,lost", [
+    (1, 1, 1, 0.3, 0.1, 0.2, "closest"),     # mostly empty regions and orders
+    (2, 3, 8, 9.5, 0.95, 9.9, "cost"),       # max SKUs (a mask unit spans every uniform of a
+                                             # round) and rates near the multiplication method's
+                                             # limit: long units, many carried products
+    (16, 9, 4, 6.0, 0.5, 7.5, "shipment"),   # widest group (16 warehouses per env)
+])
+def test_demand_and_allocation_edges_vs_oracle(W, R, K, lo, p, lq, lost):
+    cfg = make_synthetic_env_config(W, R, K, episode_length=15, lambda_orders=lo, probability_skus=p,
+                                    lambda_quantity=lq, lost_sales=lost)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 192, 32, seed=11, check_every=4)
