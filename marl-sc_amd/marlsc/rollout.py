@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 from typing import Any, Dict, Optional
 
@@ -47,6 +48,35 @@ class MLP(nn.Sequential):
         if config.get("output_activation"):
             layers.append(_act(config["output_activation"]))
         super().__init__(*layers)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return mlp_forward(self, x)
+
+
+# Inference (no autograd) runs each Linear -> ReLU pair as one GEMM with the ReLU in the GEMM
+# epilogue (torch._addmm_activation -> hipBLASLt), instead of a GEMM plus a separate elementwise
+# pass over the [N, hidden] activations. MSC_FUSED_MLP=0 restores the plain layer sequence.
+_FUSED = os.environ.get("MSC_FUSED_MLP", "1") != "0"
+
+
+def mlp_forward(layers, x: torch.Tensor, start: int = 0) -> torch.Tensor:
+    """layers[start:] applied to x (an nn.Sequential of Linear / activation modules)."""
+    mods = list(layers)[start:]
+    if not (_FUSED and x.is_cuda and not torch.is_grad_enabled()):
+        for m in mods:
+            x = m(x)
+        return x
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, nn.Linear) and m.bias is not None and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
+            lead = x.shape[:-1]
+            x = torch._addmm_activation(m.bias, x.reshape(-1, x.shape[-1]), m.weight.t()).reshape(*lead, -1)
+            i += 2
+        else:
+            x = m(x)
+            i += 1
+    return x
 
 
 @dataclass
@@ -117,9 +147,7 @@ def split_global_mlp(mlp: nn.Sequential, local_obs: torch.Tensor, agent: Optiona
         h = torch.nn.functional.linear(local_obs, first.weight[:, :L], first.bias) + g.unsqueeze(-2)
     else:
         h = torch.nn.functional.linear(local_obs[..., agent, :], first.weight[:, :L], first.bias) + g
-    for layer in list(mlp)[1:]:
-        h = layer(h)
-    return h
+    return mlp_forward(mlp, h, 1)
 
 
 def _vp(t: Optional[torch.Tensor]):

@@ -66,3 +66,21 @@ def test_rollout_replays_bit_exact_on_a_fresh_env():
         assert torch.equal(obs, col.obs[t])
         obs, rew, trunc, _ = env2.step(col.actions[t].clamp(-1.0, 1.0).contiguous())
         assert torch.equal(rew, col.rewards[t])
+
+
+def test_fused_linear_relu_inference_matches_layer_sequence():
+    # rollout inference runs Linear -> ReLU pairs as one GEMM with a ReLU epilogue; the plain layer
+    # sequence (autograd path, used by the learner) must agree to GEMM rounding
+    from marlsc.rollout import MLP, split_global_mlp
+    torch.manual_seed(0)
+    mlp = MLP(34 * 9, 1, {"hidden_sizes": [64, 64]}).cuda()
+    actor = MLP(34, 5, {"hidden_sizes": [256, 256]}).cuda()
+    x = torch.randn(4096, 8, 34, device="cuda")
+    with torch.no_grad():
+        fa = actor(x)
+        fc = split_global_mlp(mlp, x)
+    with torch.enable_grad():
+        pa = actor(x)
+        pc = split_global_mlp(mlp, x)
+    torch.testing.assert_close(fa, pa.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(fc, pc.detach(), rtol=1e-5, atol=1e-5)
