@@ -234,7 +234,7 @@ def main():
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "bytes_per_launch": int(bytes_dom),
-                         "note": "issue-bound (per-env serial RNG/parse chain), not HBM-bound: see valu_issue and DESIGN.md"},
+                         "note": "bound by the latency of each env's serial RNG/parse chain (not HBM, not chip issue rate): see valu_issue and DESIGN.md section 3"},
         }
         if valu is not None:
             out["roofline"]["valu_issue"] = valu
