@@ -64,9 +64,16 @@ def algorithmic_bytes(spec, mean_orders: float):
 
 
 def cpu_baseline(spec, seconds: float):
+    """The C oracle on the host's cores (<= 16 threads), plus a 1-core figure."""
+    out = _cpu_rate(spec, seconds, max(1, min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
+    one = _cpu_rate(spec, min(5.0, seconds / 3), 1)
+    out["value_1core"] = one["value"]
+    return out
+
+
+def _cpu_rate(spec, seconds: float, threads: int):
     import numpy as np
     import oracle as orc
-    threads = max(1, min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
     E = 64 * threads
     env = orc.OracleEnv(spec, E, base_seed=4321)
     env.reset()
@@ -90,8 +97,8 @@ def cpu_baseline(spec, seconds: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--envs", type=int, default=32768, help="envs per GPU")
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--regions", type=int, default=64)
