@@ -27,7 +27,8 @@
  *     (e.g. torch data_ptr()) unless the parameter name ends in `_host`.
  *   - Every call is stream-ordered on the given hipStream_t (pass 0 for the null stream); no call
  *     synchronises the device except msc_env_create / msc_env_destroy / msc_env_read_state /
- *     msc_env_write_state / msc_env_check.
+ *     msc_env_save_state / msc_env_load_state / msc_env_check / msc_env_set_timing /
+ *     msc_env_read_timing.
  *   - The library owns the env state buffers; callers own every I/O buffer.
  *   - One handle per stream / host thread; a handle is not thread-safe (like the reference object).
  *   - Layouts are row-major: actions [E][W][K] f32, obs [E][W][L] f32, rewards [E][W].
