@@ -240,6 +240,16 @@ int msc_gae(const float* rewards, const float* values, const float* next_values,
 /* In-place (A - mean) / max(1e-4, std) using stats {sum, sumsq, count} (device f64[3]). */
 int msc_adv_normalize(float* advantages, int64_t n, const double* stats, msc_stream_t stream);
 
+/* Rollout action sampling (RLlib TorchDiagGaussian, rlmodules/base.py:480-557) over N rows of K:
+ *   std = exp(max(log_std[n % log_std_rows][k], logstd_floor)) (one shared row, or one per agent
+ *   with rows n = env * W + agent), actions = mean + std * eps (eps: standard normal draws),
+ *   logp[n] = sum_k -(a - mean)^2 / (2 std^2) - log(std) - log(sqrt(2 pi)),
+ *   clipped = clip(actions, -1, 1) (what the env receives; the reference's EnvRunner clips too).
+ * All f32 device buffers: mean / eps / actions / clipped [N][K], log_std [log_std_rows][K], logp [N]. */
+int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std_rows, float logstd_floor,
+                        const float* eps, int64_t n_rows, int32_t k, float* actions, float* logp,
+                        float* clipped, msc_stream_t stream);
+
 /* Utility: SeedSequence(words).generate_state(1, uint32)[0] (numpy-compatible), on the host. */
 uint32_t msc_seedseq_u32(const uint32_t* words, int32_t n_words);
 

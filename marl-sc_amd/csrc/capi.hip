@@ -713,6 +713,17 @@ int msc_gae(const float* rewards, const float* values, const float* next_values,
   return 0;
 }
 
+int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std_rows, float logstd_floor,
+                        const float* eps, int64_t n_rows, int32_t k, float* actions, float* logp, float* clipped,
+                        msc_stream_t stream) {
+  if (!mean || !log_std || !eps || !actions || !logp || !clipped) return set_err(-1, "null argument");
+  if (n_rows < 0 || k < 1 || log_std_rows < 1)
+    return set_err(-1, "bad shape (n_rows %lld, k %d, log_std_rows %d)", (long long)n_rows, k, log_std_rows);
+  HIP_TRY(launch_gauss_sample(mean, log_std, log_std_rows, logstd_floor, eps, n_rows, k, actions, logp, clipped,
+                              (hipStream_t)stream));
+  return 0;
+}
+
 int msc_adv_normalize(float* adv, int64_t n, const double* stats, msc_stream_t stream) {
   if (!adv || !stats) return set_err(-1, "bad argument");
   HIP_TRY(launch_adv_normalize(adv, n, stats, (hipStream_t)stream));

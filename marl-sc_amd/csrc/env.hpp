@@ -122,5 +122,7 @@ hipError_t launch_gae(const float* r, const float* v, const float* nv, const uin
                       int64_t n, int32_t T, float gamma, float lam, float* adv, float* tgt, double* stats,
                       hipStream_t st);
 hipError_t launch_adv_normalize(float* adv, int64_t n, const double* stats, hipStream_t st);
+hipError_t launch_gauss_sample(const float* mean, const float* log_std, int32_t ls_rows, float floor_, const float* eps,
+                               int64_t N, int32_t K, float* act, float* logp, float* clipped, hipStream_t st);
 
 }  // namespace msc

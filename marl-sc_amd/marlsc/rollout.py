@@ -19,7 +19,6 @@ at C3); the MAPPO critic's flat input (local || global of the same env) is rebui
 from __future__ import annotations
 
 import ctypes as C
-import math
 import os
 from dataclasses import dataclass
 from typing import Any, Dict, Optional
@@ -154,6 +153,25 @@ def _vp(t: Optional[torch.Tensor]):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
+def gaussian_sample(mean: torch.Tensor, log_std: torch.Tensor, logstd_floor: float, eps: torch.Tensor,
+                    actions: torch.Tensor, logp: torch.Tensor) -> torch.Tensor:
+    """msc_gaussian_sample: actions = mean + exp(max(log_std, floor)) * eps, logp = the diagonal
+    Gaussian log-density summed over the last dim, into `actions` / `logp`; returns the [-1, 1]
+    clipped actions the env receives. mean / eps / actions [..., K], logp [...] (f32 CUDA);
+    log_std [K] (shared) or [P, K] repeating every P rows (e.g. [W, K]: one row per agent)."""
+    K = mean.shape[-1]
+    for t in (mean, eps, actions, logp):
+        assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+    assert actions.shape == mean.shape == eps.shape and logp.shape == mean.shape[:-1]
+    ls = log_std.detach().float().reshape(-1, K).contiguous()
+    assert (mean.numel() // K) % ls.shape[0] == 0
+    clipped = torch.empty_like(mean)
+    abi.check(abi.lib().msc_gaussian_sample(_vp(mean), _vp(ls), ls.shape[0], C.c_float(logstd_floor), _vp(eps),
+                                            mean.numel() // K, K, _vp(actions), _vp(logp), _vp(clipped),
+                                            C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    return clipped
+
+
 def gae(rewards, values, next_values, terminated, truncated, gamma, lam, adv=None, targets=None, stats=None):
     """msc_gae over [T, N] (values [T+1, N]); returns (adv, targets, stats [sum, sum_sq, n] f64)."""
     T, N = rewards.shape
@@ -215,12 +233,12 @@ class RolloutCollector:
             full = self._full(obs)
             mean, log_std = m.dist_inputs(obs, full)
             self.values[t] = m.values(obs, full)
-            std = log_std.exp()
-            a = mean + std * torch.randn(mean.shape, device=mean.device, generator=self._gen)
-            self.actions[t] = a
-            self.logp[t] = (-((a - mean) ** 2) / (2 * std * std) - log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+            eps = torch.randn(mean.shape, device=mean.device, generator=self._gen)
+            # sample, log-density and the env's clip in one HIP kernel (msc_gaussian_sample)
+            # log_std [E, W, K] is a broadcast of one row (shared policy) or of W rows (per agent)
+            a = gaussian_sample(mean.contiguous(), log_std[0], m.rc.logstd_floor, eps, self.actions[t], self.logp[t])
             may_end = env.may_truncate()
-            obs, rew, trunc, final_obs = env.step(a.clamp_(-1.0, 1.0))
+            obs, rew, trunc, final_obs = env.step(a)
             self.rewards[t] = rew
             self.truncated[t] = trunc.unsqueeze(-1)
             # truncation bootstrap: V(final_obs) for the envs whose episode ended at this step

@@ -84,3 +84,23 @@ def test_fused_linear_relu_inference_matches_layer_sequence():
         pc = split_global_mlp(mlp, x)
     torch.testing.assert_close(fa, pa.detach(), rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(fc, pc.detach(), rtol=1e-5, atol=1e-5)
+
+
+def test_gaussian_sample_kernel_matches_torch_formula():
+    # msc_gaussian_sample against the TorchDiagGaussian restatement in torch fp32
+    import math
+    from marlsc.rollout import gaussian_sample
+    g = torch.Generator(device="cuda").manual_seed(3)
+    mean = torch.randn(5000, 8, 5, device="cuda", generator=g)
+    log_std = torch.randn(8, 5, device="cuda", generator=g) - 2.0  # one row per agent
+    eps = torch.randn(5000, 8, 5, device="cuda", generator=g)
+    act = torch.empty_like(mean)
+    logp = torch.empty(5000, 8, device="cuda")
+    clipped = gaussian_sample(mean, log_std, -3.5, eps, act, logp)
+    ls = torch.clamp(log_std, min=-3.5)
+    std = ls.exp()
+    a = mean + std * eps
+    lp = (-((a - mean) ** 2) / (2 * std * std) - ls - 0.5 * math.log(2 * math.pi)).sum(-1)
+    torch.testing.assert_close(act, a, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(logp, lp, rtol=1e-5, atol=1e-5)
+    assert torch.equal(clipped, act.clamp(-1.0, 1.0))
