@@ -222,6 +222,14 @@ int64_t msc_env_state_bytes(const msc_env* env);
 int msc_env_save_state(const msc_env* env, void* buf_host);
 int msc_env_load_state(msc_env* env, const void* buf_host);
 
+/* Set SeedManager._episode_counter of every env (counters_host [E], host, >= 0; synchronous).
+ * Replaces the caller-side write `seed_manager._episode_counter = 0` (src/algorithms/base.py:81):
+ * the next construction-seeded reset of env i derives its episode root from
+ * SeedSequence([root_i, counters_host[i]]) (seed_manager.py:100-120), so E eval envs created with
+ * the same root and counters 0..E-1 replay the reference eval env's episodes 0..E-1, which it runs
+ * one after another with eval cycling (multi_env.py:220-224). */
+int msc_env_set_episode_counters(msc_env* env, const int32_t* counters_host);
+
 /* Synchronise and report device-side errors (order-buffer overflow, ...). */
 int msc_env_check(msc_env* env);
 
@@ -239,6 +247,20 @@ int msc_gae(const float* rewards, const float* values, const float* next_values,
 
 /* In-place (A - mean) / max(1e-4, std) using stats {sum, sumsq, count} (device f64[3]). */
 int msc_adv_normalize(float* advantages, int64_t n, const double* stats, msc_stream_t stream);
+
+/* Per-module variants (RLlib's GAE connector standardises the advantages of every module of a
+ * multi-agent batch on its own; with one policy per agent that is one group per agent):
+ * sequence n belongs to group n % n_groups (the rollout's sequences are env * W + agent, so
+ * n_groups = W gives one group per agent); n_groups in [1, 64] must divide n_seq.
+ * stats_out is device f64 [n_groups][3] {sum A, sum A^2, count} (accumulated, caller zeroes it);
+ * msc_adv_normalize_grouped standardises element i of the [T][n_seq] advantages with the
+ * statistics of group i % n_groups. n_groups = 1 is msc_gae / msc_adv_normalize. */
+int msc_gae_grouped(const float* rewards, const float* values, const float* next_values,
+                    const uint8_t* terminated, const uint8_t* truncated, int64_t n_seq, int32_t T,
+                    float gamma, float lam, float* advantages, float* targets, int32_t n_groups,
+                    double* stats_out, msc_stream_t stream);
+int msc_adv_normalize_grouped(float* advantages, int64_t n, int32_t n_groups, const double* stats,
+                              msc_stream_t stream);
 
 /* Rollout action sampling (RLlib TorchDiagGaussian, rlmodules/base.py:480-557) over N rows of K:
  *   std = exp(max(log_std[n % log_std_rows][k], logstd_floor)) (one shared row, or one per agent

@@ -704,13 +704,22 @@ int msc_env_check(msc_env* env) {
   return 0;
 }
 
+int msc_gae_grouped(const float* rewards, const float* values, const float* next_values, const uint8_t* terminated,
+                    const uint8_t* truncated, int64_t n_seq, int32_t T, float gamma, float lam, float* advantages,
+                    float* targets, int32_t n_groups, double* stats_out, msc_stream_t stream) {
+  if (!rewards || !values || !advantages || n_seq < 0 || T < 0) return set_err(-1, "bad argument");
+  if (n_groups < 1 || n_groups > 64 || n_seq % n_groups != 0)
+    return set_err(-1, "n_groups %d must be in [1, 64] and divide n_seq %lld", n_groups, (long long)n_seq);
+  HIP_TRY(launch_gae(rewards, values, next_values, terminated, truncated, n_seq, T, gamma, lam, advantages, targets,
+                     n_groups, stats_out, (hipStream_t)stream));
+  return 0;
+}
+
 int msc_gae(const float* rewards, const float* values, const float* next_values, const uint8_t* terminated,
             const uint8_t* truncated, int64_t n_seq, int32_t T, float gamma, float lam, float* advantages,
             float* targets, double* stats_out, msc_stream_t stream) {
-  if (!rewards || !values || !advantages || n_seq < 0 || T < 0) return set_err(-1, "bad argument");
-  HIP_TRY(launch_gae(rewards, values, next_values, terminated, truncated, n_seq, T, gamma, lam, advantages, targets,
-                     stats_out, (hipStream_t)stream));
-  return 0;
+  return msc_gae_grouped(rewards, values, next_values, terminated, truncated, n_seq, T, gamma, lam, advantages,
+                         targets, 1, stats_out, stream);
 }
 
 int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std_rows, float logstd_floor,
@@ -724,9 +733,26 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
   return 0;
 }
 
+int msc_adv_normalize_grouped(float* adv, int64_t n, int32_t n_groups, const double* stats, msc_stream_t stream) {
+  if (!adv || !stats || n < 0) return set_err(-1, "bad argument");
+  if (n_groups < 1 || n_groups > 64 || n % n_groups != 0)
+    return set_err(-1, "n_groups %d must be in [1, 64] and divide n %lld", n_groups, (long long)n);
+  HIP_TRY(launch_adv_normalize(adv, n, n_groups, stats, (hipStream_t)stream));
+  return 0;
+}
+
 int msc_adv_normalize(float* adv, int64_t n, const double* stats, msc_stream_t stream) {
-  if (!adv || !stats) return set_err(-1, "bad argument");
-  HIP_TRY(launch_adv_normalize(adv, n, stats, (hipStream_t)stream));
+  return msc_adv_normalize_grouped(adv, n, 1, stats, stream);
+}
+
+int msc_env_set_episode_counters(msc_env* env, const int32_t* counters_host) {
+  if (!env || !counters_host) return set_err(-1, "null argument");
+  const int64_t E = env->c.E;
+  for (int64_t i = 0; i < E; i++)
+    if (counters_host[i] < 0) return set_err(-1, "episode counter %d of env %lld is negative", counters_host[i], (long long)i);
+  HIP_TRY(hipSetDevice(env->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(env->s.counter, counters_host, sizeof(int32_t) * E, hipMemcpyHostToDevice));
   return 0;
 }
 

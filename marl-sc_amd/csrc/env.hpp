@@ -119,9 +119,9 @@ size_t demand_lds_bytes(const EnvConst& c);  // per block of the production dema
 int order_record_vec4(int K);
 // gae.hip
 hipError_t launch_gae(const float* r, const float* v, const float* nv, const uint8_t* term, const uint8_t* trunc,
-                      int64_t n, int32_t T, float gamma, float lam, float* adv, float* tgt, double* stats,
-                      hipStream_t st);
-hipError_t launch_adv_normalize(float* adv, int64_t n, const double* stats, hipStream_t st);
+                      int64_t n, int32_t T, float gamma, float lam, float* adv, float* tgt, int32_t n_groups,
+                      double* stats, hipStream_t st);
+hipError_t launch_adv_normalize(float* adv, int64_t n, int32_t n_groups, const double* stats, hipStream_t st);
 hipError_t launch_gauss_sample(const float* mean, const float* log_std, int32_t ls_rows, float floor_, const float* eps,
                                int64_t N, int32_t K, float* act, float* logp, float* clipped, hipStream_t st);
 

@@ -14,6 +14,7 @@
 namespace msc {
 
 constexpr int GAE_BS = 256;
+constexpr int GAE_MAX_GROUPS = 64;  // statistics groups (RLlib standardises per module: one per agent)
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -21,12 +22,16 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Statistics groups: sequence n (= env * W + agent in the rollout's [T][E*W] layout) belongs to
+// group n % G. G = 1 is one standardisation over the whole batch (the shared policy's single
+// module); G = W standardises every agent's advantages with its own mean / std, as RLlib's GAE
+// connector does for each module of a multi-agent batch when policies are not shared.
 __global__ __launch_bounds__(GAE_BS) void gae_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                      const float* __restrict__ nv, const uint8_t* __restrict__ term,
                                                      const uint8_t* __restrict__ trunc, int64_t N, int32_t T,
                                                      float gamma, float lam, float* __restrict__ adv,
-                                                     float* __restrict__ tgt, double* __restrict__ stats) {
-  __shared__ double red[2][GAE_BS / 64];
+                                                     float* __restrict__ tgt, int32_t G, double* __restrict__ stats) {
+  __shared__ double red[3][GAE_MAX_GROUPS];
   const int64_t n = (int64_t)blockIdx.x * GAE_BS + threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
   if (n < N) {
@@ -49,7 +54,8 @@ __global__ __launch_bounds__(GAE_BS) void gae_kernel(const float* __restrict__ r
       v_next = vt;
     }
   }
-  if (stats) {
+  if (!stats) return;
+  if (G == 1) {
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
     const int wid = threadIdx.x >> 6, ln = threadIdx.x & 63;
@@ -69,36 +75,64 @@ __global__ __launch_bounds__(GAE_BS) void gae_kernel(const float* __restrict__ r
       atomicAdd(&stats[1], a2);
       atomicAdd(&stats[2], (double)cnt * (double)T);
     }
+    return;
+  }
+  for (int g = threadIdx.x; g < G; g += GAE_BS) red[0][g] = red[1][g] = red[2][g] = 0.0;
+  __syncthreads();
+  if (n < N) {
+    const int g = (int)(n % G);
+    atomicAdd(&red[0][g], s1);
+    atomicAdd(&red[1][g], s2);
+    atomicAdd(&red[2][g], (double)T);
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < G; g += GAE_BS) {
+    if (red[2][g] > 0.0) {
+      atomicAdd(&stats[3 * g + 0], red[0][g]);
+      atomicAdd(&stats[3 * g + 1], red[1][g]);
+      atomicAdd(&stats[3 * g + 2], red[2][g]);
+    }
   }
 }
 
-__global__ void adv_norm_kernel(float* __restrict__ adv, int64_t n, const double* __restrict__ st) {
-  const double cnt = st[2] > 0 ? st[2] : 1.0;
-  const double mean = st[0] / cnt;
-  double var = st[1] / cnt - mean * mean;
-  var = var > 0 ? var : 0.0;
-  double sd = sqrt(var);
-  sd = sd > 1e-4 ? sd : 1e-4;
-  const float m = (float)mean, inv = (float)(1.0 / sd);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    adv[i] = (adv[i] - m) * inv;
+// (A - mean_g) / max(1e-4, std_g) over the [T][N] advantages; element i is sequence i % N, whose
+// group is (i % N) % G = i % G because the caller's N is a multiple of G.
+__global__ void adv_norm_kernel(float* __restrict__ adv, int64_t n, int32_t G, const double* __restrict__ st) {
+  __shared__ float mg[GAE_MAX_GROUPS], ig[GAE_MAX_GROUPS];
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    const double cnt = st[3 * g + 2] > 0 ? st[3 * g + 2] : 1.0;
+    const double mean = st[3 * g] / cnt;
+    double var = st[3 * g + 1] / cnt - mean * mean;
+    var = var > 0 ? var : 0.0;
+    double sd = sqrt(var);
+    sd = sd > 1e-4 ? sd : 1e-4;
+    mg[g] = (float)mean;
+    ig[g] = (float)(1.0 / sd);
+  }
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int g = G == 1 ? 0 : (int)(i % G);
+    adv[i] = (adv[i] - mg[g]) * ig[g];
+  }
 }
 
 hipError_t launch_gae(const float* r, const float* v, const float* nv, const uint8_t* term, const uint8_t* trunc,
-                      int64_t N, int32_t T, float gamma, float lam, float* adv, float* tgt, double* stats,
+                      int64_t N, int32_t T, float gamma, float lam, float* adv, float* tgt, int32_t G, double* stats,
                       hipStream_t st) {
   if (N == 0) return hipSuccess;
+  if (G < 1 || G > GAE_MAX_GROUPS || N % G != 0) return hipErrorInvalidValue;
   const int64_t blocks = (N + GAE_BS - 1) / GAE_BS;
   hipLaunchKernelGGL(gae_kernel, dim3((unsigned)blocks), dim3(GAE_BS), 0, st, r, v, nv, term, trunc, N, T, gamma,
-                     lam, adv, tgt, stats);
+                     lam, adv, tgt, G, stats);
   return hipGetLastError();
 }
 
-hipError_t launch_adv_normalize(float* adv, int64_t n, const double* stats, hipStream_t st) {
+hipError_t launch_adv_normalize(float* adv, int64_t n, int32_t G, const double* stats, hipStream_t st) {
   if (n == 0) return hipSuccess;
+  if (G < 1 || G > GAE_MAX_GROUPS || n % G != 0) return hipErrorInvalidValue;
   int64_t blocks = (n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(adv_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, st, adv, n, stats);
+  hipLaunchKernelGGL(adv_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, st, adv, n, G, stats);
   return hipGetLastError();
 }
 

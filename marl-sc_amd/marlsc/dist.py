@@ -5,8 +5,9 @@ Env ids: rank g owns global env ids [g*E, (g+1)*E); every env's root seed derive
 id (SeedManager.derive_env_seed(base, worker, global_id), base.py:377-431 of the reference), so an
 env's trajectory does not depend on the number of GPUs (weak scaling, no env-state exchange).
 
-Advantage normalisation: the GAE kernel accumulates [sum A, sum A^2, n] in f64 per rank; these
-24 bytes are SUM-all-reduced (RCCL over xGMI on MI355X, gloo on CPU) once per rollout, and every
+Advantage normalisation: the GAE kernel accumulates [sum A, sum A^2, n] in f64 per rank (one row
+per module: one for the shared policy, W when every agent has its own); these 24 B per module are
+SUM-all-reduced (RCCL over xGMI on MI355X, gloo on CPU) once per rollout, and every
 rank normalises with the global mean/std: (A - mean) / max(1e-4, std) (RLlib's standardisation).
 """
 from __future__ import annotations
@@ -32,9 +33,10 @@ def env_index_offset(envs_per_rank: int, rank: Optional[int] = None) -> int:
 
 
 def allreduce_adv_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
-    """In-place SUM all-reduce of the f64 [sum, sum_sq, n] advantage statistics."""
-    if stats.dtype != torch.float64 or stats.numel() != 3:
-        raise ValueError("advantage statistics must be a float64 tensor of 3 elements")
+    """In-place SUM all-reduce of the f64 [sum, sum_sq, n] advantage statistics ([3], or [G, 3]
+    with one row per module when every agent has its own policy)."""
+    if stats.dtype != torch.float64 or stats.numel() % 3 != 0 or stats.numel() == 0 or stats.shape[-1] != 3:
+        raise ValueError("advantage statistics must be a float64 tensor of shape [3] or [G, 3]")
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.SUM, group=group)
     return stats
@@ -42,7 +44,7 @@ def allreduce_adv_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
 
 def mean_std(stats: torch.Tensor) -> Tuple[float, float]:
     """Global mean and (population) std from reduced [sum, sum_sq, n]."""
-    s, ss, n = (float(v) for v in stats.tolist())
+    s, ss, n = (float(v) for v in stats.reshape(-1).tolist())
     if n <= 0:
         raise ValueError("no advantages")
     mean = s / n

@@ -112,11 +112,11 @@ def run_single(args) -> Dict[str, Any]:
                   f"eval_return={res.get('eval/episode_return_mean')} "
                   f"loss={res.get('learner/total_loss', float('nan')):.4f} ({res['time_this_iter_s']:.2f}s)",
                   flush=True)
-            if cfg.checkpoint_freq and trainer.iteration % cfg.checkpoint_freq == 0:
-                trainer.save_checkpoint(out / "checkpoints" / f"checkpoint_{trainer.iteration:06d}")
+        # every rank writes its own runtime state (env blob, generators); rank 0 the learner state
+        if cfg.checkpoint_freq and trainer.iteration % cfg.checkpoint_freq == 0:
+            trainer.save_checkpoint(out / "checkpoints" / f"checkpoint_{trainer.iteration:06d}")
         last = res
-    if rank == 0:
-        trainer.save_checkpoint(out / "checkpoints" / "checkpoint_final")
+    trainer.save_checkpoint(out / "checkpoints" / "checkpoint_final")
     return last
 
 
@@ -136,7 +136,7 @@ def run_evaluate(args) -> Dict[str, Any]:
     root_seed = meta["root_seed"] if args.root_seed is None else args.root_seed
     trainer = PPOTrainer(env_cfg, cfg, root_seed=root_seed, n_envs=1, rollout_len=1,
                          device=0 if args.device is None else args.device, env_meta=env_meta, eval_seed=args.eval_seed)
-    trainer.load_checkpoint(ckpt)
+    trainer.load_checkpoint(ckpt, runtime=False)  # weights only: evaluation builds its own envs
     n = args.eval_episodes or DEFAULT_EVAL_EPISODES
     res = trainer.evaluate(n)
     res.update({"checkpoint": str(ckpt), "root_seed": root_seed, "eval_seed": trainer.eval_seed,

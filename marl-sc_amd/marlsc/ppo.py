@@ -4,13 +4,22 @@ PyTorch-ROCm over the HIP env and the HIP GAE kernel.
 Reference behaviour restated (RLlib 2.52.1 itself is not importable here: parity unpinned; the
 tests check the loss against a direct restatement and the training loop's invariants):
 * algorithm config: src/algorithms/ippo.py / mappo.py `_build_config` -- lr, train batch, epochs,
-  minibatch = batch_size // num_minibatches, shuffled per epoch, clip_param, vf_clip_param,
-  vf_loss_coeff, entropy_coeff, grad_clip (global norm), use_kl_loss, GAE(gamma, lambda);
-  parameter sharing = one "shared_policy" module for every agent, else one module per agent
-  (mappo.py:102-113), warehouse one-hot in the observation when sharing;
-* loss: `PPOTorchLearner.compute_loss_for_module` -- clipped surrogate on exp(logp - logp_old),
-  squared value error clipped at vf_clip_param, Gaussian entropy bonus, optional KL penalty with
-  RLlib's adaptive coefficient (x1.5 above 2 kl_target, x0.5 below kl_target / 2);
+  minibatch_size = batch_size // num_minibatches (mappo.py:148), shuffled per epoch, clip_param,
+  vf_clip_param, vf_loss_coeff, entropy_coeff, grad_clip (global norm), use_kl_loss,
+  GAE(gamma, lambda); parameter sharing = one "shared_policy" module for every agent, else one
+  module per agent (mappo.py:102-113), warehouse one-hot in the observation when sharing;
+* minibatches: RLlib's MiniBatchCyclicIterator -- every module's batch (its AGENT steps: all
+  W agents' rows for the shared policy, one agent's rows per per-agent policy) is cut into
+  minibatches of minibatch_size rows, cycling through reshuffled epochs until every module has
+  covered num_epochs passes; one optimizer step per minibatch over every module at once. The
+  shared policy of W agents therefore takes W x num_minibatches steps per epoch;
+* loss: `PPOTorchLearner.compute_loss_for_module` per module -- clipped surrogate on
+  exp(logp - logp_old), squared value error clipped at vf_clip_param, Gaussian entropy bonus,
+  optional KL penalty with RLlib's adaptive coefficient (x1.5 above 2 kl_target, x0.5 below
+  kl_target / 2); the learner minimises the SUM of the module losses and clips each module's
+  gradients by its own global norm (TorchLearner.compute_gradients / postprocess_gradients);
+* advantages are standardised per module (RLlib's GAE connector): over all agents for the shared
+  policy, per agent otherwise (marlsc/rollout.py, msc_gae_grouped);
 * hysteretic weighting: src/algorithms/learners/hysteretic_learner.py:35-42 -- negative
   advantages scaled by hysteretic_beta before the loss;
 * learning-rate schedules: [[timestep, lr], ...] piecewise linear in sampled env steps;
@@ -27,6 +36,7 @@ from __future__ import annotations
 import json
 import math
 import os
+from collections import deque
 from dataclasses import asdict, dataclass, field
 from pathlib import Path
 from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
@@ -238,51 +248,126 @@ def allreduce_grads(params: Sequence[nn.Parameter]) -> None:
         off += n
 
 
+class _CyclicRows:
+    """One module's row stream of RLlib's MiniBatchCyclicIterator: minibatches of `mb` rows cut from
+    a shuffled pass over the module's M rows, wrapping into the next (reshuffled) pass; `covered`
+    counts the passes completed."""
+
+    def __init__(self, rows: torch.Tensor, mb: int, gen: torch.Generator):
+        self.rows, self.mb, self.gen = rows, int(mb), gen
+        self.M = rows.numel()
+        self.start, self.covered = 0, 0
+        self.perm = self._shuffle()
+
+    def _shuffle(self) -> torch.Tensor:
+        return self.rows[torch.randperm(self.M, device=self.rows.device, generator=self.gen)]
+
+    def next(self) -> torch.Tensor:
+        parts, start, stop = [], self.start, self.start + self.mb
+        while stop >= self.M:
+            parts.append(self.perm[start:])
+            self.covered += 1
+            self.perm = self._shuffle()
+            stop -= self.M
+            start = 0
+        parts.append(self.perm[start:stop])
+        self.start = stop
+        return torch.cat(parts) if len(parts) > 1 else parts[0]
+
+
+def minibatch_rows(cfg: "PPOConfig", world: int = 1) -> int:
+    """Rows per module and minibatch on one rank: RLlib's minibatch_size = batch_size //
+    num_minibatches agent steps per module (mappo.py:148), split over the ranks that all-reduce
+    their gradients (each rank holds 1/world of the train batch)."""
+    mb = max(1, int(cfg.batch_size) // max(1, int(cfg.num_minibatches)))
+    return max(1, mb // max(1, int(world)))
+
+
 class PPOLearner:
-    """Minibatch SGD over one collected batch (num_epochs x num_minibatches, shuffled per epoch)."""
+    """Minibatch SGD over one collected batch, module by module as RLlib's learner does."""
+
+    @property
+    def kl_coeff(self) -> float:
+        return float(np.mean(self.kl_coeffs))
 
     def __init__(self, module: MultiAgentActorCritic, cfg: PPOConfig, *, seed: int = 0):
         self.module, self.cfg = module, cfg
         self.opt = torch.optim.Adam(module.parameters(), lr=cfg.lr_at(0))
-        self.kl_coeff = float(cfg.kl_coeff)
+        # RLlib keeps one adaptive KL coefficient per module
+        self.kl_coeffs = [float(cfg.kl_coeff)] * len(module.policies)
         dev = next(module.parameters()).device
         self.gen = torch.Generator(device=dev).manual_seed(int(seed))
+        self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
 
-    def update(self, batch: Dict[str, torch.Tensor], full_fn, timestep: int) -> Dict[str, float]:
-        """batch tensors are [S, W, ...] (S = samples of one agent slot); full_fn(obs) -> flat obs."""
+    def _module_rows(self, S: int, W: int, device) -> List[torch.Tensor]:
+        """Flat row ids (s * W + w) of every module's batch: all rows for the shared policy, agent
+        w's rows for policy w."""
+        if self.module.shared:
+            return [torch.arange(S * W, device=device)]
+        return [torch.arange(S, device=device) * W + w for w in range(W)]
+
+    def _forward(self, policy: "AgentModule", obs: torch.Tensor, rows: torch.Tensor):
+        """(mean, log_std, values) of `policy` on batch rows (flat ids s * W + w of obs [S, W, L])."""
+        rc = self.module.rc
+        S, W, L = obs.shape
+        local = obs.reshape(S * W, L)[rows]
+        full = None
+        if rc.actor_obs_type == "global" or rc.critic_obs_type == "global":
+            full = torch.cat([local, obs[torch.div(rows, W, rounding_mode="floor")].reshape(-1, W * L)], dim=-1)
+        mean = policy.actor(full if rc.actor_obs_type == "global" else local)
+        log_std = torch.clamp(policy.log_std, min=rc.logstd_floor).expand_as(mean)
+        values = policy.critic(full if rc.critic_obs_type == "global" else local).squeeze(-1)
+        return mean, log_std, values
+
+    def update(self, batch: Dict[str, torch.Tensor], full_fn=None, timestep: int = 0) -> Dict[str, float]:
+        """batch tensors are [S, W, ...] (S env samples of W agents). full_fn is unused (the learner
+        gathers each row's local || global observation itself) and kept for call compatibility."""
         cfg, m = self.cfg, self.module
         for g in self.opt.param_groups:
             g["lr"] = cfg.lr_at(timestep)
-        S = batch["obs"].shape[0]
-        mb = max(1, S // max(1, cfg.num_minibatches))
+        obs = batch["obs"]
+        S, W = obs.shape[0], obs.shape[1]
+        flat = {k: v.reshape(S * W, *v.shape[2:]) for k, v in batch.items() if k != "obs"}
+        mb = minibatch_rows(cfg, self.world)
+        streams = [_CyclicRows(r, min(mb, r.numel()), self.gen) for r in self._module_rows(S, W, obs.device)]
         acc: Dict[str, float] = {}
+        kl_sum = [0.0] * len(streams)
         n = 0
-        for _ in range(cfg.num_epochs):
-            perm = torch.randperm(S, device=batch["obs"].device, generator=self.gen)
-            for i in range(0, S - mb + 1, mb):
-                idx = perm[i:i + mb]
-                b = {k: v[idx] for k, v in batch.items()}
-                full = full_fn(b["obs"]) if full_fn is not None else None
-                mean, log_std = m.dist_inputs(b["obs"], full)
-                values = m.values(b["obs"], full)
-                loss, st = ppo_loss(cfg, mean, log_std, values, b, self.kl_coeff)
-                self.opt.zero_grad(set_to_none=True)
-                loss.backward()
-                params = [p for p in m.parameters() if p.grad is not None]
-                allreduce_grads(params)
-                if cfg.grad_clip:
-                    torch.nn.utils.clip_grad_norm_(params, cfg.grad_clip)
-                self.opt.step()
-                for k, v in st.items():
-                    acc[k] = acc.get(k, 0.0) + float(v.detach())
-                n += 1
+        while min(st.covered for st in streams) < max(1, int(cfg.num_epochs)):
+            total = None
+            mstats: Dict[str, torch.Tensor] = {}
+            for j, (pol, st) in enumerate(zip(m.policies, streams)):
+                idx = st.next()
+                b = {k: v[idx] for k, v in flat.items()}
+                mean, log_std, values = self._forward(pol, obs, idx)
+                loss, sts = ppo_loss(cfg, mean, log_std, values, b, self.kl_coeffs[j])
+                total = loss if total is None else total + loss
+                if "mean_kl" in sts:
+                    kl_sum[j] += float(sts["mean_kl"].detach())
+                for k, v in sts.items():
+                    mstats[k] = mstats.get(k, 0.0) + v.detach() / len(streams)
+            self.opt.zero_grad(set_to_none=True)
+            total.backward()
+            allreduce_grads([p for p in m.parameters() if p.grad is not None])
+            if cfg.grad_clip:
+                for pol in m.policies:  # each module's gradients by its own global norm
+                    ps = [p for p in pol.parameters() if p.grad is not None]
+                    if ps:
+                        torch.nn.utils.clip_grad_norm_(ps, cfg.grad_clip)
+            self.opt.step()
+            for k, v in mstats.items():
+                acc[k] = acc.get(k, 0.0) + float(v)
+            n += 1
         out = {k: v / max(n, 1) for k, v in acc.items()}
-        if cfg.use_kl_loss and "mean_kl" in out:  # RLlib's adaptive KL coefficient
-            if out["mean_kl"] > 2.0 * cfg.kl_target:
-                self.kl_coeff *= 1.5
-            elif out["mean_kl"] < 0.5 * cfg.kl_target:
-                self.kl_coeff *= 0.5
-            out["kl_coeff"] = self.kl_coeff
+        out["num_minibatch_steps"] = n
+        if cfg.use_kl_loss:  # RLlib's adaptive KL coefficient, per module
+            for j in range(len(streams)):
+                kl = kl_sum[j] / max(n, 1)
+                if kl > 2.0 * cfg.kl_target:
+                    self.kl_coeffs[j] *= 1.5
+                elif kl < 0.5 * cfg.kl_target:
+                    self.kl_coeffs[j] *= 0.5
+            out["kl_coeff"] = float(np.mean(self.kl_coeffs))
         out["learning_rate"] = self.opt.param_groups[0]["lr"]
         return out
 
@@ -408,12 +493,18 @@ class PPOTrainer:
             for p in self.module.parameters():
                 dist.broadcast(p.data, src=0)
         self.learner = PPOLearner(self.module, cfg, seed=self.train_seed + self.rank)
-        self.collector = RolloutCollector(self.env, self.module, self.T, seed=self.train_seed + 1000 + self.rank)
+        # advantages standardised per module (RLlib's GAE connector): one group for the shared policy,
+        # one per agent otherwise
+        self.collector = RolloutCollector(self.env, self.module, self.T, seed=self.train_seed + 1000 + self.rank,
+                                          adv_groups=1 if cfg.parameter_sharing else W)
         self.env.reset()
         self.iteration = 0
         self.timesteps = 0
         self._ep_ret = torch.zeros(E, dtype=torch.float64, device=self.device)
-        self._completed: List[float] = []
+        # RLlib's metrics_num_episodes_for_smoothing = num_eval_episodes (mappo.py:177): the train
+        # return is the mean of the last num_eval_episodes completed episodes
+        self._completed: deque = deque(maxlen=max(1, int(cfg.num_eval_episodes)))
+        self._n_episodes = 0
 
     def _full_fn(self):
         if self.cfg.actor_obs_type != "global":  # the critic evaluates its split first layer
@@ -434,7 +525,9 @@ class PPOTrainer:
         for t in range(T):
             self._ep_ret += rew[t]
             if bool(trunc[t].any()):
-                self._completed.extend(self._ep_ret[trunc[t]].tolist())
+                ended = self._ep_ret[trunc[t]].tolist()
+                self._completed.extend(ended)
+                self._n_episodes += len(ended)
                 self._ep_ret[trunc[t]] = 0.0
         self.timesteps += T * E * self.world
         batch = {"obs": out["obs"].reshape(T * E, W, -1), "actions": out["actions"].reshape(T * E, W, -1),
@@ -446,24 +539,34 @@ class PPOTrainer:
             batch["mean_old"], batch["log_std_old"] = mo, lo
         stats = self.learner.update(batch, self._full_fn(), self.timesteps)
         self.iteration += 1
-        done = self._completed[-max(1, cfg.num_eval_episodes) * E:]
+        done = list(self._completed)
         res = {"training_iteration": self.iteration, "num_env_steps_sampled_lifetime": self.timesteps,
                "train/episode_return_mean": float(np.mean(done)) if done else None,
-               "train/episodes": len(self._completed)}
+               "train/episodes": self._n_episodes}
         res.update({f"learner/{k}": v for k, v in stats.items()})
         return res
 
     @torch.no_grad()
     def evaluate(self, n_episodes: Optional[int] = None, seed: Optional[int] = None) -> Dict[str, Any]:
-        """Deterministic (mean-action) episodes on fresh eval envs ('val' data mode)."""
+        """Deterministic (mean-action) evaluation episodes ('val' data mode).
+
+        The reference evaluates on ONE env built with seed=eval_seed (no per-env seed derivation in
+        'val' mode, src/algorithms/base.py:405-417) and num_eval_episodes set, running its episodes
+        one after another; reset k derives the episode root SeedSequence([eval_seed, k]) and the
+        counter cycles back to 0 after num_eval_episodes (multi_env.py:220-224). Here the n
+        episodes run side by side: n envs with root eval_seed whose episode counters start at
+        0..n-1, so env k plays exactly the reference's eval episode k."""
         from .spec import EnvSpec
         from .vec_env import VecInventoryEnv
         n = int(n_episodes or self.cfg.num_eval_episodes)
         meta = dict(self.env_meta)
         meta["data_mode"] = "val"
+        meta["num_eval_episodes"] = n
         spec = EnvSpec.from_config(self.env_config, meta)
+        root = self.eval_seed if seed is None else int(seed)
         env = VecInventoryEnv(None, n, spec=spec, device=self.device.index,
-                              base_seed=self.eval_seed if seed is None else int(seed))
+                              env_seeds=np.full(n, root & 0xFFFFFFFF, dtype=np.uint32))
+        env.set_episode_counters(np.arange(n, dtype=np.int32))
         obs = env.reset()
         full_fn = self._full_fn()
         ret = torch.zeros(n, dtype=torch.float64, device=self.device)
@@ -477,25 +580,54 @@ class PPOTrainer:
         return {"eval/episode_return_mean": float(r.mean()), "eval/episode_return_std": float(r.std()),
                 "eval/episodes": n}
 
-    # -- checkpoints (module + optimizer + counters + configs) --------------------------------
+    # -- checkpoints ------------------------------------------------------------------------------
+    # learner_state.pt (rank 0): module, optimizer, KL coefficients, counters; state.json: configs and
+    # observation statistics; runtime_rank<r>.pt (every rank): the rank's env state blob
+    # (msc_env_save_state, pending pre-generated demand included), its current observations, the
+    # rollout / learner generators and the running episode returns -- so a resumed run continues
+    # exactly where the saved one stopped instead of replaying its first iteration.
     def save_checkpoint(self, path: Union[str, Path]) -> Path:
         p = Path(path)
         p.mkdir(parents=True, exist_ok=True)
-        torch.save({"module": self.module.state_dict(), "optimizer": self.learner.opt.state_dict(),
-                    "kl_coeff": self.learner.kl_coeff, "iteration": self.iteration, "timesteps": self.timesteps},
-                   p / "learner_state.pt")
-        stats = self.env_meta.get("obs_stats")
-        (p / "state.json").write_text(json.dumps({
-            "iteration": self.iteration, "timesteps": self.timesteps, "root_seed": self.root_seed,
-            "algorithm": asdict(self.cfg),
-            "obs_stats": None if stats is None else [np.asarray(stats[0]).tolist(), np.asarray(stats[1]).tolist()]},
-            indent=1))
+        if self.rank == 0:
+            torch.save({"module": self.module.state_dict(), "optimizer": self.learner.opt.state_dict(),
+                        "kl_coeffs": list(self.learner.kl_coeffs), "iteration": self.iteration,
+                        "timesteps": self.timesteps}, p / "learner_state.pt")
+            stats = self.env_meta.get("obs_stats")
+            (p / "state.json").write_text(json.dumps({
+                "iteration": self.iteration, "timesteps": self.timesteps, "root_seed": self.root_seed,
+                "world_size": self.world, "algorithm": asdict(self.cfg),
+                "obs_stats": None if stats is None else [np.asarray(stats[0]).tolist(), np.asarray(stats[1]).tolist()]},
+                indent=1))
+        blob = self.env.save_state()
+        torch.save({"env_state": torch.frombuffer(bytearray(blob), dtype=torch.uint8),
+                    "obs": self.env.obs.detach().cpu(), "t_sync": int(getattr(self.env, "_t_sync", -1)),
+                    "rollout_gen": self.collector._gen.get_state(), "learner_gen": self.learner.gen.get_state(),
+                    "ep_ret": self._ep_ret.detach().cpu(), "completed": list(self._completed),
+                    "n_episodes": self._n_episodes}, p / f"runtime_rank{self.rank}.pt")
         return p
 
-    def load_checkpoint(self, path: Union[str, Path]) -> None:
-        st = torch.load(Path(path) / "learner_state.pt", map_location=self.device, weights_only=True)
+    def load_checkpoint(self, path: Union[str, Path], runtime: bool = True) -> None:
+        """Restore the learner (and with runtime=True this rank's env / generator state: resume)."""
+        p = Path(path)
+        st = torch.load(p / "learner_state.pt", map_location=self.device, weights_only=True)
         self.module.load_state_dict(st["module"])
         self.learner.opt.load_state_dict(st["optimizer"])
-        self.learner.kl_coeff = float(st["kl_coeff"])
+        if "kl_coeffs" in st:
+            self.learner.kl_coeffs = [float(x) for x in st["kl_coeffs"]]
+        else:  # round-1 checkpoints
+            self.learner.kl_coeffs = [float(st["kl_coeff"])] * len(self.module.policies)
         self.iteration = int(st["iteration"])
         self.timesteps = int(st["timesteps"])
+        rt_path = p / f"runtime_rank{self.rank}.pt"
+        if not runtime or not rt_path.exists():  # module-only checkpoint: weights restored, sampling restarts
+            return
+        rt = torch.load(rt_path, map_location="cpu", weights_only=True)
+        self.env.load_state(bytes(rt["env_state"].numpy().tobytes()))
+        self.env.obs.copy_(rt["obs"].to(self.device))
+        self.env._t_sync = int(rt["t_sync"])
+        self.collector._gen.set_state(rt["rollout_gen"])
+        self.learner.gen.set_state(rt["learner_gen"])
+        self._ep_ret.copy_(rt["ep_ret"].to(self.device))
+        self._completed = deque((float(x) for x in rt["completed"]), maxlen=self._completed.maxlen)
+        self._n_episodes = int(rt["n_episodes"])

@@ -172,8 +172,10 @@ def gaussian_sample(mean: torch.Tensor, log_std: torch.Tensor, logstd_floor: flo
     return clipped
 
 
-def gae(rewards, values, next_values, terminated, truncated, gamma, lam, adv=None, targets=None, stats=None):
-    """msc_gae over [T, N] (values [T+1, N]); returns (adv, targets, stats [sum, sum_sq, n] f64)."""
+def gae(rewards, values, next_values, terminated, truncated, gamma, lam, adv=None, targets=None, stats=None,
+        groups: int = 1):
+    """msc_gae_grouped over [T, N] (values [T+1, N]); returns (adv, targets, stats [groups, 3] f64 of
+    [sum, sum_sq, n] per group; sequence n belongs to group n % groups)."""
     T, N = rewards.shape
     for name, t, shape in (("rewards", rewards, (T, N)), ("values", values, (T + 1, N)),
                            ("next_values", next_values, (T, N))):
@@ -184,24 +186,35 @@ def gae(rewards, values, next_values, terminated, truncated, gamma, lam, adv=Non
             raise ValueError(f"{name}: expected contiguous uint8 {(T, N)}")
     adv = torch.empty_like(rewards) if adv is None else adv
     targets = torch.empty_like(rewards) if targets is None else targets
-    stats = torch.zeros(3, dtype=torch.float64, device=rewards.device) if stats is None else stats.zero_()
+    if stats is None:
+        stats = torch.zeros((groups, 3), dtype=torch.float64, device=rewards.device)
+    elif tuple(stats.shape) != (groups, 3) or stats.dtype != torch.float64:
+        raise ValueError(f"stats: expected float64 {(groups, 3)}")
+    else:
+        stats.zero_()
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    abi.check(abi.lib().msc_gae(_vp(rewards), _vp(values), _vp(next_values), _vp(terminated), _vp(truncated), N, T,
-                                C.c_float(gamma), C.c_float(lam), _vp(adv), _vp(targets), _vp(stats), st))
+    abi.check(abi.lib().msc_gae_grouped(_vp(rewards), _vp(values), _vp(next_values), _vp(terminated), _vp(truncated),
+                                        N, T, C.c_float(gamma), C.c_float(lam), _vp(adv), _vp(targets), int(groups),
+                                        _vp(stats), st))
     return adv, targets, stats
 
 
 def normalize_advantages(adv: torch.Tensor, stats: torch.Tensor) -> torch.Tensor:
-    """In place (A - mean) / max(1e-4, std) with the (already all-reduced) statistics."""
+    """In place (A - mean_g) / max(1e-4, std_g) with the (already all-reduced) statistics of the
+    [groups, 3] table; element i of the flattened [T, N] advantages belongs to group i % groups."""
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    abi.check(abi.lib().msc_adv_normalize(_vp(adv), adv.numel(), _vp(stats), st))
+    g = stats.numel() // 3
+    abi.check(abi.lib().msc_adv_normalize_grouped(_vp(adv), adv.numel(), g, _vp(stats), st))
     return adv
 
 
 class RolloutCollector:
-    """T steps of E envs x W agents (parameter sharing: one policy, N = E*W sequences)."""
+    """T steps of E envs x W agents (N = E*W sequences). Advantages are standardised per module as
+    RLlib's GAE connector does: over every agent for one shared policy (adv_groups = 1), per agent
+    for one policy per agent (adv_groups = W)."""
 
-    def __init__(self, env: VecInventoryEnv, module: ActorCritic, T: int, *, seed: int = 0):
+    def __init__(self, env: VecInventoryEnv, module: ActorCritic, T: int, *, seed: int = 0,
+                 adv_groups: int = 1):
         self.env, self.module, self.T = env, module, int(T)
         E, W, K, L = env.n_envs, env.W, env.K, env.local_obs_dim
         dev = env.device
@@ -216,7 +229,10 @@ class RolloutCollector:
         self.truncated = torch.zeros((T, E, W), dtype=torch.uint8, device=dev)
         self.adv = torch.empty((T, E, W), device=dev)
         self.targets = torch.empty((T, E, W), device=dev)
-        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        if adv_groups not in (1, W):
+            raise ValueError(f"adv_groups must be 1 (shared policy) or W={W} (one policy per agent)")
+        self.adv_groups = int(adv_groups)
+        self.stats = torch.zeros((self.adv_groups, 3), dtype=torch.float64, device=dev)
         self._flat = torch.empty((E, W, L * (1 + W)), device=dev)
         self._gen = torch.Generator(device=dev).manual_seed(seed)
         self._need_flat = module.rc.actor_obs_type == "global"  # the critic splits its first layer
@@ -253,7 +269,7 @@ class RolloutCollector:
         N = self.N
         gae(self.rewards.view(T, N), self.values.view(T + 1, N), self.next_values.view(T, N),
             self.terminated.view(T, N), self.truncated.view(T, N), m.rc.gamma, m.rc.lam,
-            self.adv.view(T, N), self.targets.view(T, N), self.stats)
+            self.adv.view(T, N), self.targets.view(T, N), self.stats, groups=self.adv_groups)
         if normalize:
             allreduce_adv_stats(self.stats)
             normalize_advantages(self.adv, self.stats)

@@ -186,6 +186,15 @@ class VecInventoryEnv:
         buf = (C.c_char * n).from_buffer_copy(blob)
         abi.check(abi.lib().msc_env_load_state(self._h, buf))
 
+    def set_episode_counters(self, counters) -> None:
+        """SeedManager._episode_counter of every env ([E] ints >= 0; the caller-side write of
+        src/algorithms/base.py:81): the next reset of env i starts episode counters[i] of its root
+        seed (msc_env_set_episode_counters)."""
+        arr = np.ascontiguousarray(counters, dtype=np.int32)
+        if arr.shape != (self.n_envs,):
+            raise ValueError(f"counters must have shape ({self.n_envs},), got {arr.shape}")
+        abi.check(abi.lib().msc_env_set_episode_counters(self._h, arr.ctypes.data_as(C.c_void_p)))
+
     def check(self) -> None:
         abi.check(abi.lib().msc_env_check(self._h))
 

@@ -3,7 +3,8 @@
 The reference delegates GAE to RLlib 2.52.1 (not vendored, not installed: parity unpinned
 against RLlib itself). This restates the textbook GAE(gamma, lambda) with RLlib's conventions:
 terminated -> bootstrap 0, truncated -> bootstrap V(terminal obs), value targets = A + V,
-then (A - mean) / max(1e-4, std) over the whole batch."""
+then (A - mean) / max(1e-4, std) over each module's batch: the whole batch for one shared policy,
+every agent's column (sequence n % W) on its own for one policy per agent."""
 import numpy as np
 
 
@@ -27,3 +28,11 @@ def gae(rewards, values, next_values, terminated, truncated, gamma, lam):
 
 def normalize(adv):
     return (adv - adv.mean()) / max(1e-4, adv.std())
+
+
+def normalize_grouped(adv, groups):
+    """adv [T, N]; sequence n standardised with the statistics of group n % groups."""
+    out = np.empty_like(adv, dtype=np.float64)
+    for g in range(groups):
+        out[:, g::groups] = normalize(adv[:, g::groups])
+    return out

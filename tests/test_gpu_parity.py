@@ -219,6 +219,44 @@ def test_gae_kernel_vs_numpy():
     np.testing.assert_allclose(_np(adv), normalize(a_ref), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("groups", [1, 8])
+def test_grouped_gae_statistics_vs_numpy(groups):
+    # per-module standardisation (RLlib's GAE connector, one module per agent when not sharing):
+    # sequence n = env * W + agent belongs to group n % W; agents get different advantage scales
+    import ctypes as C
+    from gae_ref import gae, normalize_grouped
+    from marlsc import abi
+    rng = np.random.default_rng(1)
+    T, W, E = 40, 8, 300
+    N = E * W
+    scale = np.tile(np.arange(1, W + 1, dtype=np.float32) ** 2, E)  # agent w's rewards x (w+1)^2
+    r = (rng.normal(size=(T, N)) * scale + scale).astype(np.float32)
+    v = rng.normal(size=(T + 1, N)).astype(np.float32)
+    nv = rng.normal(size=(T, N)).astype(np.float32)
+    te = np.zeros((T, N), np.uint8)
+    tr = np.zeros((T, N), np.uint8)
+    tr[17] = 1
+    dev = {k: torch.from_numpy(x).cuda() for k, x in dict(r=r, v=v, nv=nv, te=te, tr=tr).items()}
+    adv = torch.empty((T, N), device="cuda")
+    tgt = torch.empty((T, N), device="cuda")
+    stats = torch.zeros((groups, 3), dtype=torch.float64, device="cuda")
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    abi.check(abi.lib().msc_gae_grouped(p(dev["r"]), p(dev["v"]), p(dev["nv"]), p(dev["te"]), p(dev["tr"]), N, T,
+                                        C.c_float(0.99), C.c_float(0.95), p(adv), p(tgt), groups, p(stats), None))
+    a_ref, _ = gae(r.astype(np.float64), v.astype(np.float64), nv.astype(np.float64), te, tr, 0.99, 0.95)
+    s = _np(stats)
+    for g in range(groups):
+        assert s[g, 2] == T * N // groups
+        np.testing.assert_allclose(s[g, 0], a_ref[:, g::groups].sum(), rtol=1e-5)
+        np.testing.assert_allclose(s[g, 1], (a_ref[:, g::groups] ** 2).sum(), rtol=1e-5)
+    abi.check(abi.lib().msc_adv_normalize_grouped(p(adv), T * N, groups, p(stats), None))
+    np.testing.assert_allclose(_np(adv), normalize_grouped(a_ref, groups), rtol=1e-3, atol=1e-3)
+    # an n_groups that does not divide the sequence count is refused, not silently misread
+    with pytest.raises(RuntimeError):
+        abi.check(abi.lib().msc_gae_grouped(p(dev["r"]), p(dev["v"]), p(dev["nv"]), p(dev["te"]), p(dev["tr"]), N, T,
+                                            C.c_float(0.99), C.c_float(0.95), p(adv), p(tgt), 7, p(stats), None))
+
+
 def test_pettingzoo_adapter_matches_golden():
     from marlsc.env import InventoryEnvironment
     d, meta = load("repo_3wh5sku")

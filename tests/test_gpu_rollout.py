@@ -42,8 +42,8 @@ def test_rollout_buffers_gae_and_normalisation(critic_obs):
     np.testing.assert_allclose(col.adv.view(T, N).cpu().numpy(), a_ref, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(col.targets.view(T, N).cpu().numpy(), t_ref, rtol=1e-4, atol=1e-4)
     s = col.stats.cpu().numpy()
-    assert s[2] == T * N
-    np.testing.assert_allclose(s[0], a_ref.sum(), rtol=1e-5)
+    assert s.shape == (1, 3) and s[0, 2] == T * N
+    np.testing.assert_allclose(s[0, 0], a_ref.sum(), rtol=1e-5)
     from marlsc.rollout import normalize_advantages
     normalize_advantages(col.adv, col.stats)
     np.testing.assert_allclose(col.adv.view(T, N).cpu().numpy(), norm_np(a_ref), rtol=1e-3, atol=1e-3)

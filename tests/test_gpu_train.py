@@ -101,3 +101,81 @@ def test_experiment_cli_single_then_evaluate(tmp_path):
                  "--eval-episodes", "3", "--root-seed", "42"]) == 0
     res = json.loads((out / "eval_results.json").read_text())
     assert res["eval/episodes"] == 3 and res["iteration"] == 2
+
+
+def test_eval_envs_replay_the_reference_eval_episodes():
+    # The reference evaluates on ONE env seeded with eval_seed (no per-env derivation in 'val'
+    # mode, src/algorithms/base.py:405-417), episodes one after another: reset k starts episode
+    # root SeedSequence([eval_seed, k]). evaluate() runs them side by side; env k must start
+    # exactly where the reference's k-th sequential reset does (checked on the C oracle env).
+    import oracle as orc
+    from marlsc import make_synthetic_env_config
+    from marlsc.spec import EnvSpec
+    from marlsc.vec_env import VecInventoryEnv
+    cfg = make_synthetic_env_config(3, 6, 2, episode_length=9)
+    n, eval_seed = 5, 987654321
+    spec = EnvSpec.from_config(cfg, {"data_mode": "val", "num_eval_episodes": n})
+    gpu = VecInventoryEnv(None, n, spec=spec, device=0, env_seeds=np.full(n, eval_seed, np.uint32))
+    gpu.set_episode_counters(np.arange(n))
+    obs = gpu.reset().cpu().numpy()
+    sg = gpu.read_state()
+    ref = orc.OracleEnv(spec, 1, env_seeds=[eval_seed])
+    for k in range(n):
+        o = ref.reset()
+        sr = ref.read_state()
+        np.testing.assert_array_equal(obs[k], o[0])
+        np.testing.assert_array_equal(sg["inventory"][k], sr["inventory"][0])
+        np.testing.assert_array_equal(sg["rng"][k], sr["rng"][0])
+        assert sg["episode_counter"][k] == k + 1 == sr["episode_counter"][0]
+    gpu.close()
+
+
+def test_resume_from_checkpoint_continues_the_saved_run(tmp_path):
+    # resume = the uninterrupted run: the env state (pending pre-generated demand included), the
+    # observations, the rollout / learner generators and the episode-return buffers are restored,
+    # so iteration k+1 after a resume samples exactly what the uninterrupted run samples
+    from marlsc.ppo import PPOTrainer
+    tr, env_cfg, cfg = _trainer("mappo", True, E=64, T=6)
+    tr.train_iteration()
+    ck = tr.save_checkpoint(tmp_path / "ck")
+    res_a = tr.train_iteration()
+    st_a = tr.env.read_state()
+    obs_a = tr.collector.obs.clone()
+    tr2 = PPOTrainer(env_cfg, cfg, root_seed=7, n_envs=64, rollout_len=6, device=0)
+    tr2.load_checkpoint(ck)
+    res_b = tr2.train_iteration()
+    st_b = tr2.env.read_state()
+    for k in ("inventory", "timestep", "episode_counter", "rng"):
+        np.testing.assert_array_equal(st_a[k], st_b[k])
+    assert torch.equal(obs_a, tr2.collector.obs)  # the same sampled trajectory
+    assert res_a["train/episodes"] == res_b["train/episodes"]
+    assert res_a["num_env_steps_sampled_lifetime"] == res_b["num_env_steps_sampled_lifetime"]
+    for p, q in zip(tr.module.parameters(), tr2.module.parameters()):  # f64 atomics in the GAE
+        torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)       # statistics: last-bit noise
+    # a fresh trainer WITHOUT the runtime state replays iteration 1's samples: different data
+    tr3 = PPOTrainer(env_cfg, cfg, root_seed=7, n_envs=64, rollout_len=6, device=0)
+    tr3.load_checkpoint(ck, runtime=False)
+    tr3.train_iteration()
+    assert not torch.equal(obs_a, tr3.collector.obs)
+
+
+def test_train_return_is_smoothed_over_num_eval_episodes():
+    # metrics_num_episodes_for_smoothing = num_eval_episodes (mappo.py:177)
+    tr, _, cfg = _trainer("ippo", False, E=32, T=12)
+    res = tr.train_iteration()
+    assert len(tr._completed) == cfg.num_eval_episodes and res["train/episodes"] == 32
+    rew = tr.collector.rewards.double().sum(-1)  # [T, E]; every env's first episode ends at t = 9
+    ep = rew[:10].sum(0).cpu().numpy()
+    np.testing.assert_allclose(res["train/episode_return_mean"], ep[-cfg.num_eval_episodes:].mean(), rtol=1e-12)
+
+
+def test_per_agent_policies_standardise_advantages_per_agent():
+    # one policy per agent: RLlib standardises every module's advantages on its own
+    tr, _, _ = _trainer("ippo", False, E=64, T=10)
+    tr.collector.collect(normalize=True)
+    W = tr.env.W
+    adv = tr.collector.adv.reshape(-1, W).double()
+    assert tr.collector.stats.shape == (W, 3)
+    torch.testing.assert_close(adv.mean(0), torch.zeros(W, dtype=torch.float64, device=adv.device), atol=1e-4, rtol=0)
+    torch.testing.assert_close(adv.std(0, unbiased=False), torch.ones(W, dtype=torch.float64, device=adv.device),
+                               atol=1e-3, rtol=0)

@@ -220,3 +220,82 @@ def test_split_first_layer_critic_equals_the_flat_input_critic():
         obs = torch.randn(6, W, L, dtype=torch.float64)
         full = torch.cat([obs, obs.reshape(6, 1, W * L).expand(6, W, W * L)], -1)
         torch.testing.assert_close(m.values(obs), m.values(obs, full), rtol=1e-12, atol=1e-12)
+
+
+def test_cyclic_minibatch_rows_cover_every_row_once_per_pass():
+    # RLlib's MiniBatchCyclicIterator: minibatches wrap into the next reshuffled pass
+    from marlsc.ppo import _CyclicRows
+    g = torch.Generator().manual_seed(0)
+    rows = torch.arange(10) * 3 + 1
+    st = _CyclicRows(rows, 4, g)
+    seen = []
+    while st.covered < 3:
+        idx = st.next()
+        assert idx.numel() == 4
+        seen.append(idx)
+    flat = torch.cat(seen)
+    assert flat.numel() == 32 and st.covered == 3  # ceil(3 passes x 10 rows / 4) minibatches
+    for p in range(3):  # the first 30 rows are three permutations of the module's rows
+        assert sorted(flat[10 * p:10 * (p + 1)].tolist()) == sorted(rows.tolist())
+
+
+@pytest.mark.parametrize("shared", [True, False])
+def test_minibatch_steps_per_epoch_follow_rllib_agent_step_sizing(shared):
+    # minibatch_size = batch_size // num_minibatches AGENT steps per module (mappo.py:148): the
+    # shared policy's batch holds W rows per env step, so it takes W x num_minibatches steps per
+    # epoch; each per-agent policy holds one row per env step: num_minibatches steps per epoch
+    from marlsc.ppo import MultiAgentActorCritic, PPOLearner
+    cfg = _cfg("ippo")
+    cfg.num_epochs, cfg.num_minibatches, cfg.grad_clip = 3, 4, None
+    W, L, K, S = 4, 5, 2, 64
+    cfg.batch_size = S  # one env step per sample
+    rc = cfg.rollout_config()
+    torch.manual_seed(0)
+    m = MultiAgentActorCritic(W, L, L * W, K, rc, shared)
+    obs = torch.randn(S, W, L)
+    batch = {"obs": obs, "actions": torch.randn(S, W, K), "logp": torch.randn(S, W) - 3,
+             "advantages": torch.randn(S, W), "value_targets": torch.randn(S, W)}
+    out = PPOLearner(m, cfg, seed=0).update(batch)
+    per_epoch = (W if shared else 1) * cfg.num_minibatches
+    assert out["num_minibatch_steps"] == cfg.num_epochs * per_epoch
+
+
+def test_per_agent_modules_update_independently_of_other_agents_data():
+    # one policy per agent: the learner minimises the SUM of the module losses and clips each
+    # module's gradients by its own norm (RLlib TorchLearner), so agent 0's policy update does not
+    # depend on agent 1's batch at all -- not even through a shared gradient-norm clip (the
+    # advantages of agent 1 are 1000x larger in the second run)
+    from marlsc.ppo import MultiAgentActorCritic, PPOLearner
+    cfg = _cfg("ippo")
+    cfg.num_epochs, cfg.num_minibatches, cfg.grad_clip, cfg.batch_size = 2, 2, 0.5, 32
+    W, L, K, S = 2, 6, 3, 32
+    rc = cfg.rollout_config()
+    g = torch.Generator().manual_seed(4)
+    obs = torch.randn(S, W, L, generator=g)
+    base = {"obs": obs, "actions": torch.randn(S, W, K, generator=g), "logp": torch.randn(S, W, generator=g) - 3,
+            "advantages": torch.randn(S, W, generator=g), "value_targets": torch.randn(S, W, generator=g)}
+    params = []
+    for scale in (1.0, 1000.0):
+        torch.manual_seed(9)
+        m = MultiAgentActorCritic(W, L, L * W, K, rc, False)
+        b = dict(base)
+        adv = base["advantages"].clone()
+        adv[:, 1] *= scale
+        b["advantages"] = adv
+        PPOLearner(m, cfg, seed=0).update(b)
+        params.append([p.detach().clone() for p in m.policies[0].parameters()])
+    for a, c in zip(*params):
+        torch.testing.assert_close(a, c, rtol=0, atol=0)
+
+
+def test_grouped_advantage_standardisation_restatement():
+    # per-module standardisation of the numpy oracle (tests the checker the GPU tests use):
+    # with agents' advantages on very different scales every agent ends with mean 0 / std 1
+    from gae_ref import normalize_grouped
+    g = np.random.default_rng(2)
+    T, E, W = 30, 50, 2
+    adv = g.normal(size=(T, E * W)) * np.tile([1.0, 300.0], E) + np.tile([5.0, -40.0], E)
+    out = normalize_grouped(adv, W)
+    for w in range(W):
+        col = out[:, w::W]
+        assert abs(col.mean()) < 1e-9 and abs(col.std() - 1.0) < 1e-9
