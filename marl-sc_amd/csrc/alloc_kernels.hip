@@ -1,0 +1,441 @@
+// alloc_kernels.hip -- phase B of InventoryEnvironment.step with one env per lane: the greedy
+// allocation (GreedyDemandAllocator.allocate, demand_allocator.py:118-217), the inventory update
+// (multi_env.py:307), the lost-sales handlers (lost_sales_handler.py:71-210) folded into the
+// penalty cost, the outbound cost (reward_calculator.py:143-150) and the home-region features of
+// _update_observations (multi_env.py:767-773).
+//
+// Thread mapping: lane = env, 64 envs per wave, one wave per block. The reference walks each
+// env's order list sequentially (an order's ranking and fills depend on the inventory the previous
+// order left), so every env is one dependent chain; giving each chain one lane (instead of one
+// lane per warehouse) makes the per-order bookkeeping (record unpack, ranking weight, unfulfilled
+// demand, region epilogue) one instruction for 64 envs instead of one per 8, i.e. ~10x fewer
+// wave-instructions per order than the group-per-env step_b_kernel (kept for A/B:
+// MSC_ALLOC_IMPL=group).
+//
+// Per lane: the current order's W ranking costs and the K-bit per-SKU stock masks (bit w of
+// stock[s] <=> warehouse w holds SKU s) live in registers; everything indexed by the warehouse a
+// fill lands on (inventory, shipped home, outbound cost, shipped-to-region) lives in LDS at
+// [index][lane], so a lane-varying warehouse index is one conflict-free LDS access. Order records
+// ([order][NV][E], env fastest: one 1-KiB coalesced load per wave per order) arrive in windows of
+// AL_CH orders: the next window's loads are in flight in registers while the current one is read
+// from LDS (a register FIFO rotated every order would wait on its newest load at each shift).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "env.hpp"
+#include "kcommon.hpp"
+
+namespace msc {
+
+#ifndef MSC_AL_CH
+#define MSC_AL_CH 8  // order records per window: window k + 1 is in flight (registers) while window k
+                     // is allocated from LDS
+#endif
+constexpr int AL_CH = MSC_AL_CH;
+#ifndef MSC_AL_PRIO
+#define MSC_AL_PRIO 3  // s_setprio: the step chain is the critical path next to the demand waves
+#endif
+
+// LDS layout of one block (64 envs); word offsets
+struct AlLds {
+  int rec, inv, shh, qs, out, pen, tab, hm, cl, total;  // rec: uint4, out / pen: doubles, tab: double2
+  __host__ __device__ static AlLds make(int MW, int K, int R, bool tab) {
+    AlLds L{};
+    int o = 0;
+    L.rec = o; o += AL_CH * ((1 + K + 7) / 8) * 64 * 4;  // [j][v][lane] order-record window
+    L.inv = o; o += MW * K * 64;   // [w*K+s][lane] inventory
+    L.shh = o; o += MW * K * 64;   // [w*K+s][lane] shipped by w to its home region
+    L.qs = o;  o += MW * 64;       // [w][lane] units shipped by w to the current region
+    o = (o + 3) & ~3;
+    L.out = o; o += MW * 64 * 2;   // [w][lane] outbound cost (f64)
+    L.pen = o; o += MW * 64 * 2;   // [w][lane] penalty cost (f64)
+    L.tab = o; o += tab ? R * MW * 4 : 0;  // [r][w] {of, ov} (f64 pairs)
+    L.hm = o;  o += R;             // [r] home mask
+    L.cl = o;  o += R;             // [r] closest warehouse
+    L.total = o;
+    return L;
+  }
+};
+// cost table in LDS up to this size (C3: 8 KiB; C5 16 x 256: 64 KiB -> read from L2 instead)
+constexpr size_t AL_TAB_MAX = 32 * 1024;
+
+template <int K, int MW, bool DBG, bool TAB>
+__global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  const int W = c.W, R = c.R, WK = W * K;
+  const int64_t E = c.E;
+  const int lane = threadIdx.x;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const bool ev = e < E;
+  const msc_step_info info = io.info;
+  constexpr bool dbg = DBG;
+  constexpr int NVR = Rec<K>::NV;
+  if (MSC_AL_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_AL_PRIO);
+
+  extern __shared__ __attribute__((aligned(16))) int32_t al_lds[];
+  const AlLds L = AlLds::make(MW, K, R, TAB);
+  int32_t* Linv = al_lds + L.inv + lane;
+  int32_t* Lshh = al_lds + L.shh + lane;
+  uint4* Lrec = reinterpret_cast<uint4*>(al_lds + L.rec) + lane;
+  double* Lout = reinterpret_cast<double*>(al_lds + L.out) + lane;
+  double* Lpen = reinterpret_cast<double*>(al_lds + L.pen) + lane;
+  int32_t* Lqs = al_lds + L.qs + lane;
+  // pointers used inside the order loop, read once (the loop stores to global memory, so fields
+  // read through `s` would be re-loaded after every store)
+  MSC_GLOBAL int32_t* const incp = gp(s.inc);
+  const double2* Ltab = TAB ? reinterpret_cast<const double2*>(al_lds + L.tab) : nullptr;
+  const uint32_t* Lhm = reinterpret_cast<const uint32_t*>(al_lds + L.hm);
+  const int32_t* Lcl = al_lds + L.cl;
+  {
+    double2* tw_ = reinterpret_cast<double2*>(al_lds + L.tab);
+    if constexpr (TAB) {
+      for (int i = lane; i < R * MW; i += 64) {
+        const int r = i / MW, w = i % MW;
+        tw_[i] = w < W ? make_double2(c.ofT[r * W + w], c.ovT[r * W + w]) : make_double2(0.0, 0.0);
+      }
+    }
+    uint32_t* hm_ = reinterpret_cast<uint32_t*>(al_lds + L.hm);
+    int32_t* cl_ = al_lds + L.cl;
+    for (int i = lane; i < R; i += 64) {
+      hm_[i] = c.home_mask[i];
+      cl_[i] = c.closest[i];
+    }
+  }
+  auto tab_at = [&](int r, int w) -> double2 {
+    if constexpr (TAB) return Ltab[r * MW + w];
+    else return make_double2(gp(c.ofT)[r * W + w], gp(c.ovT)[r * W + w]);
+  };
+
+  // inventory after step_a's arrivals -> LDS; per-SKU stock masks
+  uint32_t stock[K];
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) stock[sk] = 0u;
+#pragma unroll
+  for (int w = 0; w < MW; w++) {
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      const int v = (ev && w < W) ? gp(s.inv)[(int64_t)i * E + e] : 0;
+      Linv[i * 64] = v;
+      Lshh[i * 64] = 0;
+      stock[sk] |= v > 0 ? (1u << w) : 0u;
+    }
+    Lout[w * 64] = 0.0;
+    Lpen[w * 64] = 0.0;
+    Lqs[w * 64] = 0;
+  }
+  __syncthreads();  // tables
+
+  // this lane's order list: record (n, v) at base + n * nstep + v * vstep (uint4 units)
+  int n_orders = 0;
+  int64_t base = 0, nstep, vstep;
+  if (c.demand_type == MSC_DEMAND_EMPIRICAL) {
+    if (ev) {
+      const int64_t row = s.emp_start[e] + (s.t[e] % c.T);
+      const int64_t off = c.tr_off[row];
+      n_orders = (int)(c.tr_off[row + 1] - off);
+      base = off * NVR;
+    }
+    nstep = NVR;
+    vstep = 1;
+  } else {
+    n_orders = ev ? s.n_orders[e] : 0;
+    base = ev ? e : 0;
+    nstep = (int64_t)NVR * E;
+    vstep = E;
+  }
+  const MSC_GLOBAL uint4* src = gp(c.demand_type == MSC_DEMAND_EMPIRICAL ? c.tr_rec : s.orders);
+  if (dbg && ev && info.n_orders) info.n_orders[e] = n_orders;
+  int wmax = n_orders;  // orders of the wave's busiest env
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int v = __shfl_xor(wmax, o);
+    wmax = v > wmax ? v : wmax;
+  }
+
+  const int maxwh = c.max_wh, lost_type = c.lost_type, pps = c.pen_per_sku;
+  const double alpha = sgpr_d(c.alpha);
+  double skw[K], penk[K];
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) {
+    skw[sk] = sgpr_d(c.skw[sk]);
+    penk[sk] = sgpr_d(pps ? c.pen[sk] : c.pen_scalar);
+  }
+
+  int cur = -1, lost_cnt = 0;
+  uint32_t hm = 0;     // warehouses whose home region is the current region
+  uint32_t smask = 0;  // warehouses that shipped to the current region
+  int rtot = 0;        // units shipped to the current region
+  int u[K], dsum[K];
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
+
+  // region epilogue (lost_sales_handler.py:71-210 into the penalty; home-region features). Only
+  // nonzero shares are visited: the closest warehouse's, or those of the warehouses that shipped to
+  // the region (a bit loop: most iterations end some lane's region, so this runs nearly every order)
+  auto add_pen = [&](int w, double wt, double upen) {
+    Lpen[w * 64] += wt * upen;
+    if (dbg && info.lost_sales)
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) info.lost_sales[e * WK + w * K + sk] += wt * (double)u[sk];
+  };
+  auto finalize = [&](int r) {
+    if (lost_cnt > 0) {
+      double upen = 0.0;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) upen += pps ? (double)u[sk] * penk[sk] : ((double)u[sk] * skw[sk]) * penk[sk];
+      if (lost_type == MSC_LOST_COST) {  // softmax(-(of * lost_orders + ov * lost_weight) / alpha)
+        double lw = 0.0;
+#pragma unroll
+        for (int sk = 0; sk < K; sk++) lw += (double)u[sk] * skw[sk];
+        double lg[16], mx = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+          lg[w] = -INFINITY;
+          if (w < MW && w < W) {
+            const double2 t = tab_at(r, w);
+            lg[w] = -(t.x * (double)lost_cnt + t.y * lw) / alpha;
+            mx = lg[w] > mx ? lg[w] : mx;
+          }
+        }
+        double ex[16];
+#pragma unroll
+        for (int w = 0; w < 16; w++) ex[w] = (w < MW && w < W) ? exp(lg[w] - mx) : 0.0;
+        const double sum = np_sum_f64_16(ex, W);
+#pragma unroll
+        for (int w = 0; w < MW; w++) {
+          const double wt = w < W ? ex[w] / sum : 0.0;
+          if (wt != 0.0) add_pen(w, wt, upen);
+        }
+      } else if (lost_type == MSC_LOST_SHIPMENT && rtot > 0) {
+        // shares of the units shipped to the region (integer-valued: the integer sum is the f64 sum
+        // exactly; x * (1 / tot) is within an ulp of x / tot)
+        const double dt = (double)rtot;
+        for (uint32_t m = smask; m != 0u; m &= m - 1u) {
+          const int w = __builtin_ctz(m);
+          add_pen(w, (double)Lqs[w * 64] / dt, upen);
+        }
+      } else {  // closest warehouse (also shipment with nothing shipped); 1.0 * x == x
+        add_pen(Lcl[r], 1.0, upen);
+      }
+    }
+    for (uint32_t m = smask; m != 0u; m &= m - 1u) Lqs[__builtin_ctz(m) * 64] = 0;
+    // a home region: its demand is the incoming home demand of its warehouses (multi_env.py:767-769;
+    // step_a zeroed s.inc, so a home region without orders leaves 0)
+    for (uint32_t m = hm; m != 0u; m &= m - 1u) {
+      const int w = __builtin_ctz(m);
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) incp[(int64_t)(w * K + sk) * E + e] = dsum[sk];
+    }
+    if (dbg) {
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {
+        if (info.demand_per_region) info.demand_per_region[(e * R + r) * K + sk] = dsum[sk];
+        if (info.unfulfilled_demands) info.unfulfilled_demands[(e * R + r) * K + sk] = u[sk];
+      }
+      if (info.lost_order_counts) info.lost_order_counts[e * R + r] = lost_cnt;
+    }
+  };
+
+  // order-record windows: window k in LDS, window k + 1 in flight in registers
+  uint4 nxt[AL_CH][NVR];
+  auto fetch = [&](int win) {
+#pragma unroll
+    for (int j = 0; j < AL_CH; j++) {
+      const int oi = win * AL_CH + j;
+#pragma unroll
+      for (int v = 0; v < NVR; v++)
+        nxt[j][v] = oi < n_orders ? gload4(src, base + oi * nstep + v * vstep) : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto publish = [&]() {
+#pragma unroll
+    for (int j = 0; j < AL_CH; j++)
+#pragma unroll
+      for (int v = 0; v < NVR; v++) Lrec[(j * NVR + v) * 64] = nxt[j][v];
+  };
+  fetch(0);
+  publish();
+  fetch(1);
+
+  for (int oi = 0; oi <= wmax; oi++) {
+    const int jw = oi % AL_CH;
+    if (jw == 0 && oi > 0) {  // wave-uniform: window oi / AL_CH is due, start the one after
+      publish();
+      fetch(oi / AL_CH + 1);
+    }
+    union {
+      uint4 v[NVR];
+      uint16_t h[8 * NVR];
+    } ur;
+#pragma unroll
+    for (int v = 0; v < NVR; v++) ur.v[v] = Lrec[(jw * NVR + v) * 64];
+    const int r = oi < n_orders ? (int)ur.h[0] : -1;
+    if (r != cur) {  // region boundary (orders are region-major) or end of this env's list
+#ifndef MSC_AL_ABL_NOFIN  // (timing ablation only: results wrong)
+      if (cur >= 0) finalize(cur);
+#endif
+      cur = r;
+      lost_cnt = 0;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
+      hm = r >= 0 ? Lhm[r] : 0u;
+      smask = 0u;
+      rtot = 0;
+    }
+    if (oi >= n_orders) continue;
+    int d[K], rem[K];
+    bool any_d = false;
+    double tw = 0.0;  // order.sku_demands.dot(sku_weights) (demand_allocator.py:167)
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      d[sk] = ur.h[1 + sk];
+      rem[sk] = d[sk];
+      dsum[sk] += d[sk];
+      any_d |= d[sk] > 0;
+      tw += (double)d[sk] * skw[sk];
+    }
+    if (!any_d) continue;  // an empty order ships nothing and is never lost
+    // demand_allocator.py:168-172; every row is read first (unconditionally: the LDS table is
+    // padded to MW, the global one clamped), so the loads overlap instead of each waiting alone
+    double2 trow[MW];
+#pragma unroll
+    for (int w = 0; w < MW; w++) trow[w] = tab_at(r, TAB ? w : (w < W ? w : W - 1));
+    double cost[MW];
+#pragma unroll
+    for (int w = 0; w < MW; w++) cost[w] = w < W ? trow[w].x + trow[w].y * tw : INFINITY;
+    int used = 0;
+    for (;;) {
+      // candidates: warehouses holding a still-needed SKU (a warehouse that shipped already has
+      // nothing left the order needs: fill = min(rem, inv) zeroes one of the two for every SKU;
+      // a warehouse with nothing to give is skipped without counting towards max_splits)
+      uint32_t cand = 0u;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) cand |= rem[sk] > 0 ? stock[sk] : 0u;
+      if (cand == 0u) break;
+      // cheapest candidate, lowest index on ties (the stable argsort order the fixtures assert)
+      double best = INFINITY;
+      int b = 0;
+#pragma unroll
+      for (int w = 0; w < MW; w++) {
+        const bool take = ((cand >> w) & 1u) && cost[w] < best;
+        best = take ? cost[w] : best;
+        b = take ? w : b;
+      }
+      // every LDS value of warehouse b is read in one batch (one wait), then written back: shipped
+      // home is accumulated unconditionally (+0 when r is not b's home region)
+      int iv[K], sh[K];
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {
+        iv[sk] = Linv[(b * K + sk) * 64];
+        sh[sk] = Lshh[(b * K + sk) * 64];
+      }
+      const bool home_b = (hm >> b) & 1u;
+      const double out_b = Lout[b * 64];
+      const int qs_b = Lqs[b * 64];
+      const double2 tb = tab_at(r, b);
+      int f[K], fs = 0;
+      double fw = 0.0;
+      bool done = true;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {
+        f[sk] = rem[sk] < iv[sk] ? rem[sk] : iv[sk];
+        const int left = iv[sk] - f[sk];
+        stock[sk] &= left > 0 ? ~0u : ~(1u << b);
+        rem[sk] -= f[sk];
+        done &= rem[sk] <= 0;
+        fs += f[sk];
+        fw += (double)f[sk] * skw[sk];
+        Linv[(b * K + sk) * 64] = left;
+        Lshh[(b * K + sk) * 64] = sh[sk] + (home_b ? f[sk] : 0);
+      }
+      // outbound cost of this shipment; the whole order from here: the ranking cost bit for bit
+      const double oc = fw == tw ? best : tb.x + tb.y * fw;
+      Lout[b * 64] = out_b + oc;
+      Lqs[b * 64] = qs_b + fs;
+      smask |= 1u << b;
+      rtot += fs;
+      if (dbg) {
+#pragma unroll
+        for (int sk = 0; sk < K; sk++) {
+          if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + b) * R + r) * K + sk] += f[sk];
+          if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + b * K + sk] += f[sk];
+        }
+        if (info.shipment_counts) info.shipment_counts[(e * W + b) * R + r] += 1;
+        if (info.shipment_quantities) info.shipment_quantities[(e * W + b) * R + r] += fs;
+      }
+      used++;
+#ifdef MSC_AL_ABL_ONEROUND  // (timing ablation only: results wrong)
+      break;
+#endif
+      if (done || used >= maxwh) break;
+    }
+    bool anyrem = false;
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      anyrem |= rem[sk] > 0;
+      u[sk] += rem[sk] > 0 ? rem[sk] : 0;
+    }
+    lost_cnt += anyrem ? 1 : 0;
+  }
+
+  if (!ev) return;
+#pragma unroll
+  for (int w = 0; w < MW; w++) {
+    if (w >= W) break;
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      const int64_t g = (int64_t)i * E + e;
+      const int left = Linv[i * 64];
+      s.sc_sht[g] = s.inv[g] - left;  // shipped this step = the inventory drop (only shipments lower it here)
+      s.inv[g] = left;
+      s.sc_shh[g] = Lshh[i * 64];
+    }
+    s.sc_pen[w * E + e] = Lpen[w * 64];
+    s.sc_out[w * E + e] = Lout[w * 64];
+  }
+}
+
+size_t alloc_lane_lds_bytes(const EnvConst& c, int MW) {
+  const bool tab = (size_t)c.R * MW * 16 <= AL_TAB_MAX;
+  return (size_t)AlLds::make(MW, c.K, c.R, tab).total * sizeof(int32_t);
+}
+
+template <int K, int MW>
+static void launch_alloc_mw(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
+  using KFn = void (*)(const DevEnv*, StepIO);
+  const bool tab = (size_t)c.R * MW * 16 <= AL_TAB_MAX;
+  const bool dbg = io.has_info != 0;
+  KFn f = dbg ? (tab ? (KFn)alloc_lane_kernel<K, MW, true, true> : (KFn)alloc_lane_kernel<K, MW, true, false>)
+              : (tab ? (KFn)alloc_lane_kernel<K, MW, false, true> : (KFn)alloc_lane_kernel<K, MW, false, false>);
+  hipLaunchKernelGGL(f, dim3((unsigned)((c.E + 63) / 64)), dim3(64), alloc_lane_lds_bytes(c, MW), st, d, io);
+}
+
+template <int K>
+void launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
+  if (c.W <= 4)
+    launch_alloc_mw<K, 4>(c, d, io, st);
+  else if (c.W <= 8)
+    launch_alloc_mw<K, 8>(c, d, io, st);
+  else
+    launch_alloc_mw<K, 16>(c, d, io, st);
+}
+
+hipError_t launch_alloc_lane(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
+  switch (c.K) {
+    case 1: launch_alloc_lane_k<1>(c, d, io, st); break;
+    case 2: launch_alloc_lane_k<2>(c, d, io, st); break;
+    case 3: launch_alloc_lane_k<3>(c, d, io, st); break;
+    case 4: launch_alloc_lane_k<4>(c, d, io, st); break;
+    case 5: launch_alloc_lane_k<5>(c, d, io, st); break;
+    case 6: launch_alloc_lane_k<6>(c, d, io, st); break;
+    case 7: launch_alloc_lane_k<7>(c, d, io, st); break;
+    case 8: launch_alloc_lane_k<8>(c, d, io, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace msc

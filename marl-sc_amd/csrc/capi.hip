@@ -243,6 +243,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     // step_c observation staging when the block's stage fits (C3: 8 x 64 x 35 floats = 70 KiB)
     c.obs_stage = (size_t)c.W * BS * (c.L + 1) * sizeof(float) <= 80 * 1024 ? 1 : 0;
     if (const char* os = getenv("MSC_OBS_STAGE")) c.obs_stage = c.obs_stage && atoi(os) != 0;
+    const char* al = getenv("MSC_ALLOC_IMPL");
+    c.alloc_impl = al && strcmp(al, "group") == 0 ? 1 : 0;
   }
 
   TablePack tp;

@@ -34,6 +34,7 @@ struct EnvConst {
   int32_t parser_rot;   // which wave of a demand block parses: (wave + rot(block)) % (1 + G) == 0 (A/B knob)
   int32_t obs_stage;    // 1: step_c stages each wave's observations in LDS and writes them coalesced
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
+  int32_t alloc_impl;   // phase B: 0 = one env per lane (alloc_lane_kernel, default); 1 = one env per lane group (step_b_kernel, A/B)
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;
@@ -114,6 +115,8 @@ hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask,
                         int32_t flags, float* obs, hipStream_t st);
 hipError_t launch_step(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen_demand, hipStream_t st);
 hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st);
+// alloc_kernels.hip
+hipError_t launch_alloc_lane(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
 hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hipStream_t st);
 size_t demand_lds_bytes(const EnvConst& c);  // per block of the production demand kernel
 int order_record_vec4(int K);

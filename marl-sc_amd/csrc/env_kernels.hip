@@ -15,6 +15,7 @@
 #include <math.h>
 
 #include "env.hpp"
+#include "kcommon.hpp"
 #include "rng.hpp"
 
 namespace msc {
@@ -35,34 +36,6 @@ __device__ unsigned long long g_prof[16];
 #define PROF_ADD(v, x)
 #define PROF_FLUSH(i, v)
 #endif
-
-// Explicit global address space for hot buffers: pointers loaded from the device-resident DevEnv
-// are generic, and generic (flat_*) loads also count against lgkmcnt, so any LDS wait would also
-// wait for them and defeat software prefetching.
-#define MSC_GLOBAL __attribute__((address_space(1)))
-template <typename T>
-__device__ __forceinline__ MSC_GLOBAL T* gp(T* p) {
-  return (MSC_GLOBAL T*)p;
-}
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // uint4 as a native vector type
-__device__ __forceinline__ uint4 gload4(const MSC_GLOBAL uint4* p, int64_t i) {
-  const v4u v = reinterpret_cast<const MSC_GLOBAL v4u*>(p)[i];
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void gstore4(MSC_GLOBAL uint4* p, int64_t i, uint4 x) {
-  v4u v;
-  v.x = x.x; v.y = x.y; v.z = x.z; v.w = x.w;
-  reinterpret_cast<MSC_GLOBAL v4u*>(p)[i] = v;
-}
-
-// ------------------------------------------------------------------------------------------
-// small helpers
-// ------------------------------------------------------------------------------------------
-template <int K>
-struct Rec {
-  static constexpr int NV = (1 + K + 7) / 8;  // uint4 words per order record
-  uint16_t h[8 * NV];
-};
 
 template <int K>
 __device__ __forceinline__ void load_rec(const uint4* p, int64_t stride, int& region, int (&q)[K]) {
@@ -870,24 +843,6 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
 // every phase its own natural thread mapping; the phases exchange ~0.7 KB per env through HBM
 // scratch (EnvState::sc_*), and [i][E] state stays coalesced for the wave = warehouse phases.
 // ------------------------------------------------------------------------------------------
-// numpy pairwise sum (add.reduce, n <= 16): sequential below 8 elements, else 8 accumulators
-// (static indices only: v stays in registers)
-__device__ __forceinline__ double np_sum_f64_16(const double (&v)[16], int n) {
-  if (n < 8) {
-    double r = 0.0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) r = i < n ? r + v[i] : r;
-    return r;
-  }
-  double a[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++) a[j] = n >= 16 ? v[j] + v[8 + j] : v[j];
-  double r = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-#pragma unroll
-  for (int i = 8; i < 16; i++) r = (n < 16 && i < n) ? r + v[i] : r;
-  return r;
-}
-
 // ---- phase A ------------------------------------------------------------------------------
 template <int K, bool DBG>
 __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __restrict__ dp, StepIO io) {
@@ -1072,13 +1027,6 @@ __device__ __forceinline__ double group_np_sum(double v, int n) {
 #ifndef MSC_SB_WPE
 #define MSC_SB_WPE 5
 #endif
-
-// a wave-uniform double kept in scalar registers
-__device__ __forceinline__ double sgpr_d(double v) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
 
 template <int K, int GW, bool DBG, bool TAB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
@@ -1609,7 +1557,10 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
 #undef MSC_SB
   const size_t lds_a = c.lead_type == MSC_LEAD_STOCHASTIC ? (size_t)c.W * K * BS * sizeof(int32_t) : 0;
   hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * c.W), lds_a, st, d, io);
-  hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
+  if (c.alloc_impl == 0)
+    (void)launch_alloc_lane(c, d, io, st);
+  else
+    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
   const size_t lds_c = (size_t)c.W * BS * sizeof(double) + (c.obs_stage ? (size_t)c.W * BS * (c.L + 1) * sizeof(float) : 0);
   hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), lds_c, st, d, io);
   return hipGetLastError();

@@ -1,0 +1,61 @@
+// kcommon.hpp -- small device helpers shared by the kernel translation units of libmarlsc
+// (env_kernels.hip, alloc_kernels.hip). Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace msc {
+
+// Explicit global address space for hot buffers: pointers loaded from the device-resident DevEnv
+// are generic, and generic (flat_*) loads also count against lgkmcnt, so any LDS wait would also
+// wait for them and defeat software prefetching.
+#define MSC_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ MSC_GLOBAL T* gp(T* p) {
+  return (MSC_GLOBAL T*)p;
+}
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // uint4 as a native vector type
+__device__ __forceinline__ uint4 gload4(const MSC_GLOBAL uint4* p, int64_t i) {
+  const v4u v = reinterpret_cast<const MSC_GLOBAL v4u*>(p)[i];
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gstore4(MSC_GLOBAL uint4* p, int64_t i, uint4 x) {
+  v4u v;
+  v.x = x.x; v.y = x.y; v.z = x.z; v.w = x.w;
+  reinterpret_cast<MSC_GLOBAL v4u*>(p)[i] = v;
+}
+
+// one order record of the per-step order buffer: 16-bit fields {region, q_0, ..., q_{K-1}}
+// packed into NV uint4 words, stored [order][NV][E] (env fastest)
+template <int K>
+struct Rec {
+  static constexpr int NV = (1 + K + 7) / 8;  // uint4 words per order record
+  uint16_t h[8 * NV];
+};
+
+// a wave-uniform double kept in scalar registers
+__device__ __forceinline__ double sgpr_d(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// numpy pairwise sum (add.reduce, n <= 16): sequential below 8 elements, else 8 accumulators
+// (static indices only: v stays in registers)
+__device__ __forceinline__ double np_sum_f64_16(const double (&v)[16], int n) {
+  if (n < 8) {
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r = i < n ? r + v[i] : r;
+    return r;
+  }
+  double a[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) a[j] = n >= 16 ? v[j] + v[8 + j] : v[j];
+  double r = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+  for (int i = 8; i < 16; i++) r = (n < 16 && i < n) ? r + v[i] : r;
+  return r;
+}
+
+}  // namespace msc
