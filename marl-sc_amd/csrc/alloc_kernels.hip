@@ -39,12 +39,12 @@ constexpr int AL_CH = MSC_AL_CH;
 // LDS layout of one block (64 envs); word offsets
 struct AlLds {
   int rec, inv, shh, qs, out, pen, tab, hm, cl, total;  // rec: uint4, out / pen: doubles, tab: double2
-  __host__ __device__ static AlLds make(int MW, int K, int R, bool tab) {
+  __host__ __device__ static AlLds make(int MW, int K, int R, bool tab, bool SH) {
     AlLds L{};
     int o = 0;
     L.rec = o; o += AL_CH * ((1 + K + 7) / 8) * 64 * 4;  // [j][v][lane] order-record window
     L.inv = o; o += MW * K * 64;   // [w*K+s][lane] inventory
-    L.shh = o; o += MW * K * 64;   // [w*K+s][lane] shipped by w to its home region
+    L.shh = o; o += SH ? MW * K * 64 : 0;  // [w*K+s][lane] shipped home (only when home regions are shared)
     L.qs = o;  o += MW * 64;       // [w][lane] units shipped by w to the current region
     o = (o + 3) & ~3;
     L.out = o; o += MW * 64 * 2;   // [w][lane] outbound cost (f64)
@@ -59,7 +59,7 @@ struct AlLds {
 // cost table in LDS up to this size (C3: 8 KiB; C5 16 x 256: 64 KiB -> read from L2 instead)
 constexpr size_t AL_TAB_MAX = 32 * 1024;
 
-template <int K, int MW, bool DBG, bool TAB>
+template <int K, int MW, bool DBG, bool TAB, bool SH>
 __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
   if (MSC_AL_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_AL_PRIO);
 
   extern __shared__ __attribute__((aligned(16))) int32_t al_lds[];
-  const AlLds L = AlLds::make(MW, K, R, TAB);
+  const AlLds L = AlLds::make(MW, K, R, TAB, SH);
   int32_t* Linv = al_lds + L.inv + lane;
   int32_t* Lshh = al_lds + L.shh + lane;
   uint4* Lrec = reinterpret_cast<uint4*>(al_lds + L.rec) + lane;
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
       const int i = w * K + sk;
       const int v = (ev && w < W) ? gp(s.inv)[(int64_t)i * E + e] : 0;
       Linv[i * 64] = v;
-      Lshh[i * 64] = 0;
+      if (SH) Lshh[i * 64] = 0;
       stock[sk] |= v > 0 ? (1u << w) : 0u;
     }
     Lout[w * 64] = 0.0;
@@ -165,11 +165,17 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
 
   int cur = -1, lost_cnt = 0;
   uint32_t hm = 0;     // warehouses whose home region is the current region
+  int hw = -1;         // the one warehouse whose home it is (!SH: every region is home to at most one)
   uint32_t smask = 0;  // warehouses that shipped to the current region
   int rtot = 0;        // units shipped to the current region
-  int u[K], dsum[K];
+  int u[K], dsum[K], shc[K];  // shc: shipped by hw to its home region (!SH)
 #pragma unroll
-  for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
+  for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = shc[sk] = 0;
+  // shipped home (multi_env.py:770-773) is stored when the home region ends; zero for a home region
+  // without orders
+  MSC_GLOBAL int32_t* const shhp = gp(s.sc_shh);
+  if (!SH && ev)
+    for (int i = 0; i < WK; i++) shhp[(int64_t)i * E + e] = 0;
 
   // region epilogue (lost_sales_handler.py:71-210 into the penalty; home-region features). Only
   // nonzero shares are visited: the closest warehouse's, or those of the warehouses that shipped to
@@ -221,6 +227,9 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
       }
     }
     for (uint32_t m = smask; m != 0u; m &= m - 1u) Lqs[__builtin_ctz(m) * 64] = 0;
+    if (!SH && hw >= 0)
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) shhp[(int64_t)(hw * K + sk) * E + e] = shc[sk];
     // a home region: its demand is the incoming home demand of its warehouses (multi_env.py:767-769;
     // step_a zeroed s.inc, so a home region without orders leaves 0)
     for (uint32_t m = hm; m != 0u; m &= m - 1u) {
@@ -281,8 +290,11 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
 #pragma unroll
       for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
       hm = r >= 0 ? Lhm[r] : 0u;
+      hw = hm != 0u ? __builtin_ctz(hm) : -1;
       smask = 0u;
       rtot = 0;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) shc[sk] = 0;
     }
     if (oi >= n_orders) continue;
     int d[K], rem[K];
@@ -329,7 +341,7 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
 #pragma unroll
       for (int sk = 0; sk < K; sk++) {
         iv[sk] = Linv[(b * K + sk) * 64];
-        sh[sk] = Lshh[(b * K + sk) * 64];
+        sh[sk] = SH ? Lshh[(b * K + sk) * 64] : 0;
       }
       const bool home_b = (hm >> b) & 1u;
       const double out_b = Lout[b * 64];
@@ -348,7 +360,8 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
         fs += f[sk];
         fw += (double)f[sk] * skw[sk];
         Linv[(b * K + sk) * 64] = left;
-        Lshh[(b * K + sk) * 64] = sh[sk] + (home_b ? f[sk] : 0);
+        if (SH) Lshh[(b * K + sk) * 64] = sh[sk] + (home_b ? f[sk] : 0);
+        else shc[sk] += home_b ? f[sk] : 0;
       }
       // outbound cost of this shipment; the whole order from here: the ranking cost bit for bit
       const double oc = fw == tw ? best : tb.x + tb.y * fw;
@@ -391,16 +404,20 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
       const int left = Linv[i * 64];
       s.sc_sht[g] = s.inv[g] - left;  // shipped this step = the inventory drop (only shipments lower it here)
       s.inv[g] = left;
-      s.sc_shh[g] = Lshh[i * 64];
+      if (SH) s.sc_shh[g] = Lshh[i * 64];
     }
     s.sc_pen[w * E + e] = Lpen[w * 64];
     s.sc_out[w * E + e] = Lout[w * 64];
   }
 }
 
+// shared home regions (a region that is home to two or more warehouses: possible when
+// n_regions < n_warehouses) need the LDS shipped-home table; otherwise it stays in registers, which
+// keeps the block at <= 39 KiB of LDS so two allocation blocks fit beside two demand blocks per CU
+static bool shared_homes(const EnvConst& c) { return c.shared_home != 0; }
 size_t alloc_lane_lds_bytes(const EnvConst& c, int MW) {
   const bool tab = (size_t)c.R * MW * 16 <= AL_TAB_MAX;
-  return (size_t)AlLds::make(MW, c.K, c.R, tab).total * sizeof(int32_t);
+  return (size_t)AlLds::make(MW, c.K, c.R, tab, shared_homes(c)).total * sizeof(int32_t);
 }
 
 template <int K, int MW>
@@ -408,8 +425,13 @@ static void launch_alloc_mw(const EnvConst& c, const DevEnv* d, const StepIO& io
   using KFn = void (*)(const DevEnv*, StepIO);
   const bool tab = (size_t)c.R * MW * 16 <= AL_TAB_MAX;
   const bool dbg = io.has_info != 0;
-  KFn f = dbg ? (tab ? (KFn)alloc_lane_kernel<K, MW, true, true> : (KFn)alloc_lane_kernel<K, MW, true, false>)
-              : (tab ? (KFn)alloc_lane_kernel<K, MW, false, true> : (KFn)alloc_lane_kernel<K, MW, false, false>);
+  KFn f;
+  if (shared_homes(c))
+    f = dbg ? (tab ? (KFn)alloc_lane_kernel<K, MW, true, true, true> : (KFn)alloc_lane_kernel<K, MW, true, false, true>)
+            : (tab ? (KFn)alloc_lane_kernel<K, MW, false, true, true> : (KFn)alloc_lane_kernel<K, MW, false, false, true>);
+  else
+    f = dbg ? (tab ? (KFn)alloc_lane_kernel<K, MW, true, true, false> : (KFn)alloc_lane_kernel<K, MW, true, false, false>)
+            : (tab ? (KFn)alloc_lane_kernel<K, MW, false, true, false> : (KFn)alloc_lane_kernel<K, MW, false, false, false>);
   hipLaunchKernelGGL(f, dim3((unsigned)((c.E + 63) / 64)), dim3(64), alloc_lane_lds_bytes(c, MW), st, d, io);
 }
 

@@ -175,6 +175,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     home_mask[b] |= 1u << w;
     home_of[w] = b;
   }
+  c.shared_home = 0;
+  for (int r = 0; r < R; r++) c.shared_home |= __builtin_popcount(home_mask[r]) > 1 ? 1 : 0;
   for (int r = 0; r < R; r++) {  // argmin over warehouses, lost_sales_handler.py:36
     int b = 0;
     for (int w = 1; w < W; w++)

@@ -34,6 +34,7 @@ struct EnvConst {
   int32_t parser_rot;   // which wave of a demand block parses: (wave + rot(block)) % (1 + G) == 0 (A/B knob)
   int32_t obs_stage;    // 1: step_c stages each wave's observations in LDS and writes them coalesced
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
+  int32_t shared_home;  // 1: some region is the home region of two or more warehouses
   int32_t alloc_impl;   // phase B: 0 = one env per lane (alloc_lane_kernel, default); 1 = one env per lane group (step_b_kernel, A/B)
   uint32_t flags;
   int64_t E;

@@ -9,6 +9,7 @@ torch = pytest.importorskip("torch")
 import oracle as orc  # noqa: E402
 from golden_util import COST_KEYS, ENV_FIXTURES, INFO_MAP, load, spec_of  # noqa: E402
 from marlsc import make_synthetic_env_config  # noqa: E402
+from marlsc.synthetic import FEATURE_CONFIG_YAML  # noqa: E402
 from marlsc.spec import EnvSpec  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -341,3 +342,31 @@ def test_demand_and_allocation_edges_vs_oracle(W, R, K, lo, p, lq, lost):
                                     lambda_quantity=lq, lost_sales=lost)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     _lockstep(spec, 192, 32, seed=11, check_every=4)
+
+
+@pytest.mark.parametrize("lost", ["shipment", "closest"])
+def test_shared_home_regions_vs_oracle(lost):
+    # n_regions < n_warehouses: several warehouses share a home region (multi_env.py:144), which
+    # takes the allocation kernel's LDS shipped-home path; home-region features are observed
+    feats = dict(FEATURE_CONFIG_YAML, units_shipped_home=True, incoming_demand_home=True, stockout=True)
+    cfg = make_synthetic_env_config(8, 4, 3, episode_length=20, features=feats, lost_sales=lost)
+    homes = np.argmin(np.array(cfg["cost_structure"]["distances"]), axis=1)
+    assert len(set(homes.tolist())) < len(homes), "config must share home regions"
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 192, 25, seed=8, check_every=4)
+
+
+def test_home_features_and_group_allocator_agree():
+    # the lane-per-env allocator (default) and the group-per-env one (MSC_ALLOC_IMPL=group) on the
+    # bench shape with every home-region feature observed, against the oracle
+    import os
+    feats = dict(FEATURE_CONFIG_YAML, units_shipped_home=True, incoming_demand_home=True,
+                 units_shipped_away=True, stockout=True)
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=30, features=feats)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 128, 12, seed=9, check_every=3)
+    os.environ["MSC_ALLOC_IMPL"] = "group"
+    try:
+        _lockstep(spec, 128, 12, seed=9, check_every=3)
+    finally:
+        del os.environ["MSC_ALLOC_IMPL"]
