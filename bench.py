@@ -30,10 +30,13 @@ sys.path.insert(0, str(REPO / "oracle"))
 
 BASELINE = json.loads((REPO / "BASELINE.json").read_text())
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
-# VALU issue peak: 256 CUs x 4 SIMD-32 x one wave64 instruction per 2 cycles at 2.4 GHz
-VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
+# VALU issue peak, measured (tools/ubench_isa.hip, profiles/r02/ubench_isa.txt): independent
+# v_add_u32 at 4 waves per SIMD retire one wave64 instruction per 1.78 ns per SIMD, i.e.
+# 1024 SIMDs / 1.784 ns = 574 G wave-instructions/s (integer multiplies and f64 mul/compare: 430-500)
+VALU_PEAK_WINST = 1024 / 1.784e-9
 DEMAND_KERNEL = "demand_unit_kernel"
-STEP_KERNELS = ("step_a_kernel", "step_b_kernel", "step_c_kernel")
+STEP_KERNELS = ("step_a_kernel", "alloc_lane_kernel", "step_c_kernel")
+GAE_BYTES_PER_ELEM = 4 + 4 + 4 + 1 + 1 + 4 + 4  # reward, value, next value, terminated, truncated in; advantage, target out
 
 
 def ensure_built():
@@ -190,6 +193,37 @@ def main():
             dist.barrier()
         t_roll = time.perf_counter() - t0
         env.check()
+    # (4) the HBM-bound kernel of the rollout: msc_gae (GAE reverse scan + advantage statistics) over
+    #     one MAPPO rollout's [T, E * W] sequences, timed alone with events on its stream
+    gae_line = None
+    if rank == 0 and args.rollout_T > 0:
+        from marlsc.rollout import gae
+        T, N = args.rollout_T, E * spec.W
+        gg = torch.Generator(device="cuda").manual_seed(7)
+        r_ = torch.randn((T, N), generator=gg, device="cuda")
+        v_ = torch.randn((T + 1, N), generator=gg, device="cuda")
+        nv_ = torch.randn((T, N), generator=gg, device="cuda")
+        te_ = (torch.rand((T, N), generator=gg, device="cuda") < 0.01).to(torch.uint8)
+        tr_ = torch.zeros((T, N), dtype=torch.uint8, device="cuda")
+        tr_[T - 1] = 1
+        adv_, tgt_ = torch.empty_like(r_), torch.empty_like(r_)
+        st_ = torch.zeros((1, 3), dtype=torch.float64, device="cuda")
+        for _ in range(3):
+            gae(r_, v_, nv_, te_, tr_, 0.99, 0.95, adv_, tgt_, st_)
+        reps = 20
+        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ea.record()
+        for _ in range(reps):
+            gae(r_, v_, nv_, te_, tr_, 0.99, 0.95, adv_, tgt_, st_)
+        eb.record()
+        torch.cuda.synchronize()
+        t_gae = ea.elapsed_time(eb) / 1e3 / reps
+        gb = GAE_BYTES_PER_ELEM * T * N
+        gae_line = {"kernel": "gae_kernel", "bound": "hbm", "achieved": round(gb / t_gae / 1e9, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gb / t_gae / 1e9 / HBM_PEAK_GBS, 4),
+                    "bytes_per_launch": int(gb), "ms": round(t_gae * 1e3, 4),
+                    "shape": f"T={T} x N={N} sequences (E x W of one MAPPO rollout), {GAE_BYTES_PER_ELEM} B/element"}
+        del r_, v_, nv_, te_, tr_, adv_, tgt_
     tt = torch.tensor([dt, t_roll], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -241,10 +275,12 @@ def main():
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "bytes_per_launch": int(bytes_dom),
-                         "note": "bound by the latency of each env's serial RNG/parse chain (not HBM, not chip issue rate): see valu_issue and DESIGN.md section 3"},
+                         "note": "not HBM-bound: the env step is VALU-issue-bound (PCG64 draws + the per-env parse and allocation chains); see valu_issue (measured issue peak) and DESIGN.md section 3"},
         }
         if valu is not None:
             out["roofline"]["valu_issue"] = valu
+        if gae_line is not None:
+            out["roofline_gae"] = gae_line
         if args.rollout_T > 0:
             out["rollout"] = {
                 "value": round(E * world * spec.W * args.rollout_T / t_roll, 1), "unit": "agent-steps/s",

@@ -207,6 +207,16 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       }
     }
     order_cap = (int)ceil(lam_sum + 12.0 * sqrt(lam_sum + 1.0) + 64.0);
+    // equal parameters in every region (and SKU): the demand parser's constant-threshold variant
+    c.demand_uni = 1;
+    for (int r = 0; r < R; r++) {
+      c.demand_uni &= enlam_o[r] == enlam_o[0] && p_skip[r] == p_skip[0] ? 1 : 0;
+      for (int s = 0; s < K; s++) c.demand_uni &= enlam_q[(size_t)r * K + s] == enlam_q[0] ? 1 : 0;
+    }
+    if (const char* du = getenv("MSC_DEMAND_UNI")) c.demand_uni &= atoi(du) != 0 ? 1 : 0;
+    c.uni_thr_o = enlam_o[0];
+    c.uni_thr_m = p_skip[0];
+    c.uni_thr_q = enlam_q[0];
   } else if (d->demand_type == MSC_DEMAND_EMPIRICAL) {
     const int rows = d->trace_n_rows;
     if (rows < d->episode_length) return set_err(-1, "trace has %d timesteps < episode_length %d", rows, d->episode_length);

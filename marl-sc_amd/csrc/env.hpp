@@ -35,10 +35,12 @@ struct EnvConst {
   int32_t obs_stage;    // 1: step_c stages each wave's observations in LDS and writes them coalesced
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
   int32_t shared_home;  // 1: some region is the home region of two or more warehouses
+  int32_t demand_uni;   // 1: Poisson parameters equal across regions (demand_unit_kernel<UNI>)
   int32_t alloc_impl;   // phase B: 0 = one env per lane (alloc_lane_kernel, default); 1 = one env per lane group (step_b_kernel, A/B)
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;
+  double uni_thr_o, uni_thr_m, uni_thr_q;  // demand_uni: exp(-lambda_orders), p_skip, exp(-lambda_quantity)
   const MSC_G double* act_param;   // [K]
   const MSC_G int32_t* init_vals;  // [W*K]
   const MSC_G double* hold;        // [K]

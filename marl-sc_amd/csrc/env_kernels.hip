@@ -625,7 +625,10 @@ __host__ __device__ constexpr size_t unit_lds_fixed() {
 #ifndef MSC_DEM_WPE
 #define MSC_DEM_WPE 8  // <= 64 VGPRs: two demand waves fit beside four step_b waves on a SIMD
 #endif
-template <int K, int G, bool LDS_TAB>
+// UNI: every region has the same lambda_orders, probability_skus and lambda_quantity (scalar
+// sampler parameters, demand_sampler.py:99-102, or equal per-region arrays): the three thresholds
+// live in scalar registers and the settle step needs no table reads or region-indexed addressing.
+template <int K, int G, bool LDS_TAB, bool UNI>
 __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MSC_DEM_WPE))) void demand_unit_kernel(
     const DevEnv* __restrict__ dp) {
   const EnvConst& c = dp->c;
@@ -727,6 +730,53 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   // table when a quantity unit opens, while the round's ring reads are in flight
   double tk = Tk[0], to_next = To[R > 1 ? 1 : 0];
   double prod = 1.0, thr = To[0];
+  // (scalar loads of the descriptor, consumed before the loop: a vector load here would leave its
+  // wait, vmcnt(0), inside the loop, where it also waits for every record store in flight)
+  const double u_thr_o = sgpr_d(c.uni_thr_o), u_thr_m = sgpr_d(c.uni_thr_m), u_thr_q = sgpr_d(c.uni_thr_q);
+  const int R_s = __builtin_amdgcn_readfirstlane(R), cap_s = __builtin_amdgcn_readfirstlane(cap);
+  const int64_t rstride_s = (int64_t)__builtin_amdgcn_readfirstlane((uint32_t)rstride) |
+                            ((int64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)rstride >> 32)) << 32);
+  if constexpr (UNI) thr = u_thr_o;
+  // UNI settle: the same transitions with constant thresholds
+  auto settle_uni = [&]() {
+    const int is_q = st == PS_QTY ? 1 : 0, is_o = st == PS_ORD ? 1 : 0;
+    if (is_q & (n <= cap_s ? 1 : 0)) {
+      const int h = 1 + sq;  // 16-bit field of the record (field 0 = region)
+      MSC_GLOBAL char* fp = NV == 1 ? recp + h * 2 : recp + (int64_t)(h >> 3) * E * 16 + (h & 7) * 2;
+      *reinterpret_cast<MSC_GLOBAL uint16_t*>(fp) = (uint16_t)(x > 1 ? x : 1);  // max(1, Poisson(lambda_q))
+    }
+    const unsigned m2 = is_q ? (mask & (mask - 1u)) : mask;  // a mask unit left its bits in mask
+    const int has_q = (is_o ^ 1) & (m2 != 0u ? 1 : 0);
+    const int left2 = (is_o ? x : left) - ((is_o | has_q) ^ 1);  // an order completed
+    const int new_order = (has_q ^ 1) & (left2 > 0 ? 1 : 0);
+    const int new_region = (has_q | new_order) ^ 1;
+    sq = __builtin_ctz(m2 | (1u << K));
+    st = has_q ? PS_QTY : new_order ? PS_MASK : (r + new_region < R_s ? PS_ORD : PS_DONE);
+    // three-way threshold choice as a bit select (as a ?: chain the optimizer turns it into a lookup
+    // table in scratch memory, which then keeps the whole parser state in scratch)
+    {
+      const uint64_t bo = (uint64_t)__double_as_longlong(u_thr_o), bm = (uint64_t)__double_as_longlong(u_thr_m),
+                     bq = (uint64_t)__double_as_longlong(u_thr_q);
+      const uint64_t mo = (uint64_t)0 - (uint64_t)new_order, mq = (uint64_t)0 - (uint64_t)has_q;
+      uint64_t b = bo ^ ((bo ^ bm) & mo);
+      b = b ^ ((b ^ bq) & mq);
+      thr = __longlong_as_double((long long)b);
+    }
+    mask = new_order ? 0u : m2;
+    left = left2;
+    n += new_order;
+    recp += new_order ? rstride_s : 0;
+    if (new_order & (n <= cap_s ? 1 : 0)) {
+#pragma unroll
+      for (int j = 0; j < NV; j++)
+        *reinterpret_cast<MSC_GLOBAL v4u*>(recp + (int64_t)j * E * 16) = v4u{j == 0 ? (unsigned)r : 0u, 0u, 0u, 0u};
+    }
+    r += new_region;
+    prod = 1.0;
+    x = 0;
+    mf = st == PS_MASK ? 1 : 0;
+    live = st != PS_DONE ? 1 : 0;
+  };
   // a unit ended: book its result, open the next unit (straight-line, predicated; only the two
   // record stores are guarded)
   auto settle = [&]() {
@@ -778,7 +828,11 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
       double u[UD];
 #pragma unroll
       for (int i = 0; i < UD; i++) u[i] = rp[i * BS];
-      if (pend) settle();
+      if constexpr (UNI) {
+        if (pend) settle_uni();
+      } else {
+        if (pend) settle();
+      }
       // Poisson unit: p_i = p_{i-1} * U_i in draw order; U_i < 1 makes the products non-increasing,
       // so "p_i > exp(-lambda)" holds for a leading run only and its length is a plain count.
       // Mask unit: the K Bernoulli draws, bit i = SKU drawn <=> U_i < p <=> !(U_i > p_skip).
@@ -1519,9 +1573,11 @@ static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t 
   DFn fn;
   if (c.demand_impl == 5)  // 4-draw parking parser (A/B: MSC_DEMAND_IMPL=park4)
     fn = t ? (DFn)demand_park4_kernel<K, G, true> : (DFn)demand_park4_kernel<K, G, false>;
+  else if (c.demand_uni)
+    fn = (DFn)demand_unit_kernel<K, G, false, true>;
   else
-    fn = t ? (DFn)demand_unit_kernel<K, G, true> : (DFn)demand_unit_kernel<K, G, false>;
-  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), park_fixed(c) + (t ? tab : 0), st, d);
+    fn = t ? (DFn)demand_unit_kernel<K, G, true, false> : (DFn)demand_unit_kernel<K, G, false, false>;
+  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), park_fixed(c) + (t && !c.demand_uni ? tab : 0), st, d);
 }
 
 template <int K>
