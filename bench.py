@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
 VALU_PEAK_WINST = 1024 / 1.784e-9
 DEMAND_KERNEL = "demand_unit_kernel"
 STEP_KERNELS = ("step_a_kernel", "alloc_lane_kernel", "step_c_kernel")
-GAE_BYTES_PER_ELEM = 4 + 4 + 4 + 1 + 1 + 4 + 4  # reward, value, next value, terminated, truncated in; advantage, target out
+GAE_BYTES_PER_ELEM = 4 + 4 + 1 + 1 + 4 + 4  # reward, value, terminated, truncated in; advantage, target out (next value: truncated rows only)
 
 
 def ensure_built():
@@ -219,7 +219,7 @@ def main():
         torch.cuda.synchronize()
         t_gae = ea.elapsed_time(eb) / 1e3 / reps
         gb = GAE_BYTES_PER_ELEM * T * N
-        gae_line = {"kernel": "gae_kernel", "bound": "hbm", "achieved": round(gb / t_gae / 1e9, 1),
+        gae_line = {"kernel": "gae4_kernel", "bound": "hbm", "achieved": round(gb / t_gae / 1e9, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gb / t_gae / 1e9 / HBM_PEAK_GBS, 4),
                     "bytes_per_launch": int(gb), "ms": round(t_gae * 1e3, 4),
                     "shape": f"T={T} x N={N} sequences (E x W of one MAPPO rollout), {GAE_BYTES_PER_ELEM} B/element"}

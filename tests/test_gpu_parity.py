@@ -191,12 +191,13 @@ def test_obs_flat_layout():
         np.testing.assert_array_equal(flat[:, w, spec.local_obs_dim:], loc.reshape(3, -1))
 
 
-def test_gae_kernel_vs_numpy():
+@pytest.mark.parametrize("N", [5000, 4998])  # vectorised (4 sequences per lane) and scalar kernels
+def test_gae_kernel_vs_numpy(N):
     import ctypes as C
     from gae_ref import gae, normalize
     from marlsc import abi
     rng = np.random.default_rng(0)
-    T, N = 100, 5000
+    T = 100
     r = rng.normal(size=(T, N)).astype(np.float32)
     v = rng.normal(size=(T + 1, N)).astype(np.float32)
     nv = rng.normal(size=(T, N)).astype(np.float32)
@@ -370,3 +371,35 @@ def test_home_features_and_group_allocator_agree():
         _lockstep(spec, 128, 12, seed=9, check_every=3)
     finally:
         del os.environ["MSC_ALLOC_IMPL"]
+
+
+def test_gae_vectorised_equals_scalar():
+    # the two GAE kernels do the same f32 arithmetic per element: advantages / targets bit-equal
+    import ctypes as C
+    import os
+    from marlsc import abi
+    rng = np.random.default_rng(5)
+    T, N = 37, 4096
+    dev = {"r": rng.normal(size=(T, N)), "v": rng.normal(size=(T + 1, N)), "nv": rng.normal(size=(T, N))}
+    dev = {k: torch.from_numpy(x.astype(np.float32)).cuda() for k, x in dev.items()}
+    dev["te"] = torch.from_numpy((rng.random((T, N)) < 0.05).astype(np.uint8)).cuda()
+    tr = np.zeros((T, N), np.uint8)
+    tr[11] = 1
+    tr[20, ::3] = 1
+    dev["tr"] = torch.from_numpy(tr).cuda()
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    outs = []
+    for scalar in (False, True):
+        if scalar:
+            os.environ["MSC_GAE_SCALAR"] = "1"
+        try:
+            adv, tgt = torch.empty((T, N), device="cuda"), torch.empty((T, N), device="cuda")
+            st = torch.zeros(3, dtype=torch.float64, device="cuda")
+            abi.check(abi.lib().msc_gae(p(dev["r"]), p(dev["v"]), p(dev["nv"]), p(dev["te"]), p(dev["tr"]), N, T,
+                                        C.c_float(0.99), C.c_float(0.95), p(adv), p(tgt), p(st), None))
+            torch.cuda.synchronize()
+            outs.append((adv.clone(), tgt.clone(), st.clone()))
+        finally:
+            os.environ.pop("MSC_GAE_SCALAR", None)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    np.testing.assert_allclose(_np(outs[0][2]), _np(outs[1][2]), rtol=1e-12)
