@@ -681,15 +681,11 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     int pg = g;
     auto gen_to = [&](int target) {
       while (pg < target) {
-        const double u = u64_to_double(pcg_output(th, tl));
+        const double u = pcg_output_double(th, tl);
         const int slot = pg & (UCAP - 1);
         myring[slot * BS] = u;
         myring[(slot < UD - 1 ? slot + UCAP : USLOTS - 1) * BS] = u;  // mirror (or the dummy row)
-        uint64_t nh, nl;
-        mul128(th, tl, mh, ml, nh, nl);
-        add128(nh, nl, ch, cl);
-        th = nh;
-        tl = nl;
+        lcg128(th, tl, mh, ml, ch, cl);
         pg += G;
       }
     };

@@ -134,6 +134,26 @@ MSC_HD uint64_t pcg_output(uint64_t s_hi, uint64_t s_lo) {
 }
 MSC_HD double u64_to_double(uint64_t v) { return (double)(v >> 11) * (1.0 / 9007199254740992.0); }
 
+// The same double from the state directly (XSL-RR output >> 11 as 2^-53 units): the top 32 bits of
+// the rotated word scaled by 2^-32 plus its next 21 bits scaled by 2^-53, one exact fma (the sum is
+// k * 2^-53 with k < 2^53, representable). Fewer instructions than the 64-bit shift + two
+// conversions + two scalings of u64_to_double(pcg_output(..)); bit-identical.
+MSC_HD double pcg_output_double(uint64_t s_hi, uint64_t s_lo) {
+  const uint64_t r = pcg_output(s_hi, s_lo);
+  return fma((double)(uint32_t)(r >> 32), 0x1p-32, (double)((uint32_t)r >> 11) * 0x1p-53);
+}
+
+// s <- s * m + c (mod 2^128) as one 128-bit integer expression: the backend emits the partial
+// products and a single add-with-carry chain (fewer instructions than mul128 + add128).
+MSC_HD void lcg128(uint64_t& sh, uint64_t& sl, uint64_t mh, uint64_t ml, uint64_t ch, uint64_t cl) {
+  const unsigned __int128 s = ((unsigned __int128)sh << 64) | sl;
+  const unsigned __int128 m = ((unsigned __int128)mh << 64) | ml;
+  const unsigned __int128 c = ((unsigned __int128)ch << 64) | cl;
+  const unsigned __int128 n = s * m + c;
+  sh = (uint64_t)(n >> 64);
+  sl = (uint64_t)n;
+}
+
 // Affine map s -> A*s + C of `n` PCG64 steps for increment (ih:il) (Brown, "Random number
 // generation with arbitrary strides"; numpy's pcg64_advance uses the same recurrence).
 MSC_HD void pcg_jump_coeffs(uint64_t n, uint64_t ih, uint64_t il, uint64_t& ah, uint64_t& al, uint64_t& ch,
