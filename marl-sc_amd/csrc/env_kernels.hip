@@ -612,6 +612,16 @@ constexpr int UCAP = pow2ceil(2 * UD * UHS);  // ring capacity (positions), >= 2
 constexpr int USLOTS = UCAP + UD;           // ring rows: UCAP + the UD - 1 mirrored ones + a dummy row
 static_assert((UCAP & (UCAP - 1)) == 0, "ring layout");
 
+#ifndef MSC_GEN_QUOTA
+#define MSC_GEN_QUOTA 24  // positions added per lane per chunk (mean consumption ~18 at lambda 4-5)
+#endif
+// the generators' fill target for the next phase: QUOTA more positions, capped by the ring slots the
+// parser's current chunk (starting at rdp) cannot read
+__device__ __forceinline__ int unit_quota(int tgt, int rdp) {
+  const int q = tgt + MSC_GEN_QUOTA, cap = rdp + UCAP;
+  return q < cap ? q : cap;
+}
+
 __host__ __device__ constexpr size_t unit_lds_fixed() {
   return (size_t)BS * USLOTS * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
 }
@@ -689,12 +699,25 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
         pg += G;
       }
     };
+    // Refill by quota (see unit_quota): in phase ci the parser reads positions [rdp, rdp + UHS*UD)
+    // of chunk ci, so positions up to rdp + UCAP are free; every lane gets at most QUOTA more, the
+    // same for every lane, instead of exactly what it consumed (which makes each wave loop for its
+    // busiest lane). A lane the next chunk could overrun is topped up behind one extra barrier.
+    int tgt = UCAP;
     if (valid) gen_to(UCAP);
     __syncthreads();
     for (int ci = 0;; ci++) {
-      if (valid) gen_to(rdv[(ci & 1) * BS + lane] + UCAP);
+      const int rdp = rdv[(ci & 1) * BS + lane];
+      tgt = unit_quota(tgt, rdp);
+      if (valid) gen_to(tgt);
       __syncthreads();
       if (!more[ci & 1]) break;
+      const int need = rdv[((ci + 1) & 1) * BS + lane] + UHS * UD;
+      if (__ballot(valid && tgt < need) != 0) {
+        tgt = tgt > need ? tgt : need;
+        if (valid) gen_to(tgt);
+        __syncthreads();
+      }
     }
     return;
   }
@@ -815,6 +838,7 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   PROF_DECL(n_chunk);
   PROF_DECL(p_bar);
   PROF_T(t_start);
+  int ptgt = UCAP, rd_start = 0;  // the generators' fill target and the chunk's start position
   for (int ci = 0;; ci++) {
 #pragma unroll 1
     for (int hs = 0; hs < UHS; hs++) {
@@ -859,6 +883,14 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     PROF_ADD(p_bar, PROF_NOW() - tb);
     PROF_ADD(n_chunk, 1);
     if (!any) break;
+    // the generators' refill decision, restated: their top-up barrier (if any) is joined here
+    ptgt = unit_quota(ptgt, rd_start);
+    const int need = rd + UHS * UD;
+    if (__ballot(valid && ptgt < need) != 0) {
+      ptgt = ptgt > need ? ptgt : need;
+      __syncthreads();
+    }
+    rd_start = rd;
   }
   PROF_ADD(p_all, PROF_NOW() - t_start);
   PROF_FLUSH(0, p_all);
