@@ -32,6 +32,8 @@ namespace msc {
                      // is allocated from LDS
 #endif
 constexpr int AL_CH = MSC_AL_CH;
+template <int K>
+void launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
 #ifndef MSC_AL_PRIO
 #define MSC_AL_PRIO 3  // s_setprio: the step chain is the critical path next to the demand waves
 #endif
@@ -59,11 +61,12 @@ struct AlLds {
 // cost table in LDS up to this size (C3: 8 KiB; C5 16 x 256: 64 KiB -> read from L2 instead)
 constexpr size_t AL_TAB_MAX = 32 * 1024;
 
-template <int K, int MW, bool DBG, bool TAB, bool SH>
+// EXACT: n_warehouses == MW (compile-time W: no per-warehouse `w < W` masking)
+template <int K, int MW, bool DBG, bool TAB, bool SH, bool EXACT>
 __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
-  const int W = c.W, R = c.R, WK = W * K;
+  const int W = EXACT ? MW : c.W, R = c.R, WK = W * K;
   const int64_t E = c.E;
   const int lane = threadIdx.x;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
@@ -415,36 +418,72 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
 // n_regions < n_warehouses) need the LDS shipped-home table; otherwise it stays in registers, which
 // keeps the block at <= 39 KiB of LDS so two allocation blocks fit beside two demand blocks per CU
 static bool shared_homes(const EnvConst& c) { return c.shared_home != 0; }
-size_t alloc_lane_lds_bytes(const EnvConst& c, int MW) {
+static size_t alloc_lane_lds_bytes(const EnvConst& c, int MW) {
   const bool tab = (size_t)c.R * MW * 16 <= AL_TAB_MAX;
   return (size_t)AlLds::make(MW, c.K, c.R, tab, shared_homes(c)).total * sizeof(int32_t);
 }
 
-template <int K, int MW>
+template <int K, int MW, bool EXACT>
 static void launch_alloc_mw(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   using KFn = void (*)(const DevEnv*, StepIO);
   const bool tab = (size_t)c.R * MW * 16 <= AL_TAB_MAX;
   const bool dbg = io.has_info != 0;
   KFn f;
+#define MSC_AL(DB, TB, SHV) (KFn)alloc_lane_kernel<K, MW, DB, TB, SHV, EXACT>
   if (shared_homes(c))
-    f = dbg ? (tab ? (KFn)alloc_lane_kernel<K, MW, true, true, true> : (KFn)alloc_lane_kernel<K, MW, true, false, true>)
-            : (tab ? (KFn)alloc_lane_kernel<K, MW, false, true, true> : (KFn)alloc_lane_kernel<K, MW, false, false, true>);
+    f = dbg ? (tab ? MSC_AL(true, true, true) : MSC_AL(true, false, true))
+            : (tab ? MSC_AL(false, true, true) : MSC_AL(false, false, true));
   else
-    f = dbg ? (tab ? (KFn)alloc_lane_kernel<K, MW, true, true, false> : (KFn)alloc_lane_kernel<K, MW, true, false, false>)
-            : (tab ? (KFn)alloc_lane_kernel<K, MW, false, true, false> : (KFn)alloc_lane_kernel<K, MW, false, false, false>);
+    f = dbg ? (tab ? MSC_AL(true, true, false) : MSC_AL(true, false, false))
+            : (tab ? MSC_AL(false, true, false) : MSC_AL(false, false, false));
+#undef MSC_AL
   hipLaunchKernelGGL(f, dim3((unsigned)((c.E + 63) / 64)), dim3(64), alloc_lane_lds_bytes(c, MW), st, d, io);
 }
 
 template <int K>
 void launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
-  if (c.W <= 4)
-    launch_alloc_mw<K, 4>(c, d, io, st);
-  else if (c.W <= 8)
-    launch_alloc_mw<K, 8>(c, d, io, st);
+  // exact instantiations for the warehouse counts of the BASELINE configs (2, 8, 16), masked ones
+  // (next power of two) otherwise
+  if (c.W == 2)
+    launch_alloc_mw<K, 2, true>(c, d, io, st);
+  else if (c.W <= 4)
+    launch_alloc_mw<K, 4, false>(c, d, io, st);
+  else if (c.W == 8)
+    launch_alloc_mw<K, 8, true>(c, d, io, st);
+  else if (c.W < 8)
+    launch_alloc_mw<K, 8, false>(c, d, io, st);
+  else if (c.W == 16)
+    launch_alloc_mw<K, 16, true>(c, d, io, st);
   else
-    launch_alloc_mw<K, 16>(c, d, io, st);
+    launch_alloc_mw<K, 16, false>(c, d, io, st);
 }
 
+// The SKU counts are instantiated in four translation units (MSC_AL_PART = 1..4: K 1-2, 3-4, 5-6,
+// 7-8; the Makefile compiles this file once per part) so the build runs them in parallel;
+// MSC_AL_PART 0 (a plain one-file build) instantiates all of them.
+#ifndef MSC_AL_PART
+#define MSC_AL_PART 0
+#endif
+#define MSC_AL_INST(KV) template void launch_alloc_lane_k<KV>(const EnvConst&, const DevEnv*, const StepIO&, hipStream_t);
+#if MSC_AL_PART == 0 || MSC_AL_PART == 1
+MSC_AL_INST(1)
+MSC_AL_INST(2)
+#endif
+#if MSC_AL_PART == 0 || MSC_AL_PART == 2
+MSC_AL_INST(3)
+MSC_AL_INST(4)
+#endif
+#if MSC_AL_PART == 0 || MSC_AL_PART == 3
+MSC_AL_INST(5)
+MSC_AL_INST(6)
+#endif
+#if MSC_AL_PART == 0 || MSC_AL_PART == 4
+MSC_AL_INST(7)
+MSC_AL_INST(8)
+#endif
+#undef MSC_AL_INST
+
+#if MSC_AL_PART == 0 || MSC_AL_PART == 1
 hipError_t launch_alloc_lane(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   switch (c.K) {
     case 1: launch_alloc_lane_k<1>(c, d, io, st); break;
@@ -459,5 +498,6 @@ hipError_t launch_alloc_lane(const EnvConst& c, const DevEnv* d, const StepIO& i
   }
   return hipGetLastError();
 }
+#endif
 
 }  // namespace msc
