@@ -252,6 +252,18 @@ def main():
                 valu = {"insts_per_launch": int(sum(cn)), "achieved": round(ach / 1e9, 2),
                         "peak": round(VALU_PEAK_WINST / 1e9, 1), "unit": "G wave-instructions/s",
                         "frac": round(ach / VALU_PEAK_WINST, 4)}
+        # the whole pipelined step against the same issue peak: every kernel of a step (demand of
+        # t + 1 and the step kernels of t run concurrently) over the measured time per step
+        step_valu = None
+        if tj.exists():
+            cs = tr.get("counters", {}).get(key, {})
+            names_all = (DEMAND_KERNEL,) + STEP_KERNELS
+            vals = [cs.get(n, {}).get("SQ_INSTS_VALU") for n in names_all]
+            if all(x is not None for x in vals):
+                ach_s = sum(vals) / (dt / K)
+                step_valu = {"insts_per_step": int(sum(vals)), "kernels": list(names_all),
+                             "achieved": round(ach_s / 1e9, 2), "peak": round(VALU_PEAK_WINST / 1e9, 1),
+                             "unit": "G wave-instructions/s", "frac": round(ach_s / VALU_PEAK_WINST, 4)}
         achieved = bytes_dom / t_dom / 1e9
         out = {
             "metric": BASELINE["metric"],
@@ -279,6 +291,8 @@ def main():
         }
         if valu is not None:
             out["roofline"]["valu_issue"] = valu
+        if step_valu is not None:
+            out["roofline"]["step_valu_issue"] = step_valu
         if gae_line is not None:
             out["roofline_gae"] = gae_line
         if args.rollout_T > 0:
