@@ -102,7 +102,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--envs", type=int, default=32768, help="envs per GPU")
+    ap.add_argument("--config", choices=("c3", "c5"), default="c3",
+                    help="c3: BASELINE configs[2]/[3] (8 x 64 x 5, Poisson, 32768 envs, default); c5: configs[4] "
+                         "(16 x 256 x 5, empirical trace of ~200-1,000 orders per step, 8192 envs)")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: 32768 for c3, 8192 for c5)")
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--regions", type=int, default=64)
     ap.add_argument("--skus", type=int, default=5)
@@ -134,9 +137,17 @@ def main():
     from marlsc.spec import EnvSpec
     from marlsc.vec_env import VecInventoryEnv
 
-    cfg = make_synthetic_env_config(args.agents, args.regions, args.skus)
-    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
-    E = args.envs
+    meta = {"include_warehouse_id": True}
+    if args.config == "c5":
+        from marlsc.synthetic import make_synthetic_trace
+        args.agents, args.regions, args.skus = 16, 256, 5
+        cfg = make_synthetic_env_config(16, 256, 5)
+        cfg["components"]["demand_sampler"] = {"type": "empirical", "params": None}
+        meta["demand_trace"] = make_synthetic_trace(256, 5, 300, orders_per_step=(200, 1000), seed=0)
+    else:
+        cfg = make_synthetic_env_config(args.agents, args.regions, args.skus)
+    spec = EnvSpec.from_config(cfg, meta)
+    E = args.envs if args.envs is not None else (8192 if args.config == "c5" else 32768)
     dev = torch.cuda.current_device()
     env = VecInventoryEnv(None, E, spec=spec, device=dev, base_seed=default_train_seed(42), env_index_offset=rank * E)
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
@@ -231,7 +242,8 @@ def main():
 
     if rank == 0:
         value = E * world * spec.W * K / dt
-        mean_orders = float(spec.lambda_orders.sum())
+        mean_orders = (float(spec.trace["offsets"][-1]) / spec.trace["n_rows"] if spec.demand_type == "empirical"
+                       else float(spec.lambda_orders.sum()))
         b_dem, b_step = algorithmic_bytes(spec, mean_orders)
         kern = {DEMAND_KERNEL: (t_demand, b_dem * E), "step_kernels": (t_step, b_step * E)}
         dom = max(kern, key=lambda k: kern[k][0])
@@ -277,9 +289,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32 state, u64 PCG64, f64 rewards, f32 obs",
-            "data": "synthetic (SURVEY.md 8(d) cost structure, Poisson demand lambda_o=4 p=0.667 lambda_q=5, uniform[-1,1] actions)",
+            "data": ("synthetic (SURVEY.md 8(d) cost structure, Poisson demand lambda_o=4 p=0.667 lambda_q=5, uniform[-1,1] actions)"
+                     if args.config == "c3" else
+                     f"synthetic (SURVEY.md 8(d) cost structure; empirical demand: a synthetic preprocessor frame of 300 timesteps, "
+                     f"{mean_orders:.0f} orders per step on average over 256 regions; uniform[-1,1] actions)"),
             "config": {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x "
-                                   f"{spec.K} SKUs (BASELINE configs[2]; configs[3] when N>1)",
+                                   f"{spec.K} SKUs " + ("(BASELINE configs[2]; configs[3] when N>1)" if args.config == "c3"
+                                                        else "(BASELINE configs[4], empirical trace)"),
                        "n_envs_per_gpu": E, "agents": spec.W, "regions": spec.R, "skus": spec.K,
                        "episode_length": spec.episode_length, "obs_dim_local": spec.local_obs_dim,
                        "parallelism": f"env-shard x{world}"},

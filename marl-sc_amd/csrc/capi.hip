@@ -255,8 +255,16 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     // step_c observation staging when the block's stage fits (C3: 8 x 64 x 35 floats = 70 KiB)
     c.obs_stage = (size_t)c.W * BS * (c.L + 1) * sizeof(float) <= 80 * 1024 ? 1 : 0;
     if (const char* os = getenv("MSC_OBS_STAGE")) c.obs_stage = c.obs_stage && atoi(os) != 0;
-    const char* al = getenv("MSC_ALLOC_IMPL");
-    c.alloc_impl = al && strcmp(al, "group") == 0 ? 1 : 0;
+    // phase B: one env per lane (alloc_lane_kernel) when there are enough env chains to fill the
+    // chip and the Poisson demand kernel of the next step runs beside it (it then needs the issue
+    // slots the lane kernel leaves free: C3, 32768 envs: 0.80 vs 0.86 ms/step); otherwise the
+    // group-per-env kernel, whose 8-16x more waves shorten each chain (C5, 8192 envs x 16
+    // warehouses, empirical demand: 1.08 vs 1.71 ms/step). MSC_ALLOC_IMPL=lane|group forces one.
+    c.alloc_impl = (d->demand_type == MSC_DEMAND_POISSON && n_envs >= 16384) ? 0 : 1;
+    if (const char* al = getenv("MSC_ALLOC_IMPL")) {
+      if (strcmp(al, "group") == 0) c.alloc_impl = 1;
+      else if (strcmp(al, "lane") == 0) c.alloc_impl = 0;
+    }
   }
 
   TablePack tp;

@@ -36,7 +36,7 @@ struct EnvConst {
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
   int32_t shared_home;  // 1: some region is the home region of two or more warehouses
   int32_t demand_uni;   // 1: Poisson parameters equal across regions (demand_unit_kernel<UNI>)
-  int32_t alloc_impl;   // phase B: 0 = one env per lane (alloc_lane_kernel, default); 1 = one env per lane group (step_b_kernel, A/B)
+  int32_t alloc_impl;   // phase B: 0 = one env per lane (alloc_lane_kernel); 1 = one env per lane group (step_b_kernel)
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;

@@ -7,6 +7,7 @@
 // multiplies and no 128-bit emulation library. Every function is bit-exact with numpy; the
 // parity tests compare the resulting PCG64 states after every step.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)

@@ -129,3 +129,30 @@ def make_synthetic_env_config(
         "data_source": {"type": "custom"},
         "features": dict(features if features is not None else FEATURE_CONFIG_YAML),
     }
+
+
+def make_synthetic_trace(n_regions: int, n_skus: int, n_timesteps: int = 300, orders_per_step=(200, 1000),
+                         seed: int = 0) -> Dict[str, Any]:
+    """A synthetic preprocessor output frame (src/data/preprocessor.py:682-696: timestep,
+    region_id, order_id, sku_id, quantity; one row per order line) for the empirical sampler at
+    any size (SURVEY.md 8(d), configs[4]: ~Poisson(200-1,000) orders per timestep over the
+    regions). Order ids are strings, as in the real data; an order has 1..K lines with
+    quantities 1..12. Returned as a dict of numpy columns (what `pack_demand_trace` and
+    `env_meta['demand_trace']` accept)."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    lo, hi = orders_per_step
+    n_t = rng.poisson(rng.uniform(lo, hi, n_timesteps)).astype(np.int64)   # orders per timestep
+    n = int(n_t.sum())
+    order_ts = np.repeat(np.arange(n_timesteps, dtype=np.int64), n_t)
+    order_reg = rng.integers(0, n_regions, n)
+    lines = rng.integers(1, n_skus + 1, n)                                  # distinct SKUs per order
+    # the first `lines` SKUs of a random permutation per order
+    perm = np.argsort(rng.random((n, n_skus)), axis=1)
+    take = np.arange(n_skus)[None, :] < lines[:, None]
+    o_idx, col = np.nonzero(take)
+    sku = perm[o_idx, col]
+    oid = np.char.add("o", np.char.zfill(np.arange(n).astype(str), 8))
+    return {"timestep": order_ts[o_idx], "region_id": order_reg[o_idx], "order_id": oid[o_idx],
+            "sku_id": sku.astype(np.int64), "quantity": rng.integers(1, 13, o_idx.size).astype(np.int64)}

@@ -59,3 +59,47 @@ def pack_demand_trace(src: Any, n_skus: int, data_mode: str = "train") -> Dict[s
         raise ValueError("summed order quantity exceeds 65535")
     return {"n_rows": int(len(ts_unique)), "timesteps": ts_unique, "offsets": offsets,
             "regions": regions, "quantities": quant.astype(np.int32)}
+
+
+def map_excluded_regions(order_region_ids, selected_region_ids, warehouse_to_region) -> "np.ndarray":
+    """`DataProcessor.map_excluded_regions` (src/data/preprocessor.py:382-441), restated on numpy
+    columns: an order whose region is not selected moves to the selected region that shares
+    warehouses with it and has the lowest mean `fixed_costs` over those warehouse pairs
+    (`groupby('destinationregionid').mean().idxmin()`, the smallest id among equal means); with no
+    warehouse pair for the excluded region, or no selected region served by its warehouses, it
+    moves to selected_region_ids[0]. Region ids compare as strings, as in the reference.
+
+    warehouse_to_region: dict / DataFrame with columns sourcenodeid, destinationregionid,
+    fixed_costs. Returns the mapped region ids (elements of selected_region_ids)."""
+    ids = np.asarray(order_region_ids, dtype=object)
+    sel = list(selected_region_ids)
+    sel_str = [str(r) for r in sel]
+    sel_set = set(sel_str)
+    src = np.asarray(warehouse_to_region["sourcenodeid"], dtype=object)
+    dst = np.asarray(warehouse_to_region["destinationregionid"], dtype=object).astype(str)
+    fc = np.asarray(warehouse_to_region["fixed_costs"], dtype=np.float64)
+    ids_str = ids.astype(str)
+    out = ids.copy()
+    excluded = [r for r in dict.fromkeys(ids.tolist()) if str(r) not in sel_set]  # first-seen order (unique())
+    for ex in excluded:
+        ex_s = str(ex)
+        pair = dst == ex_s
+        if not pair.any():
+            nearest = sel[0]
+        else:
+            whs = set(src[pair].tolist())
+            inc = np.isin(dst, sel_str) & np.array([w in whs for w in src.tolist()], dtype=bool)
+            if not inc.any():
+                nearest = sel[0]
+            else:
+                # mean fixed cost per destination region; pandas groups and idxmin on the original
+                # destinationregionid values; ties -> the first in sorted group order
+                keys = np.asarray(warehouse_to_region["destinationregionid"], dtype=object)[inc]
+                costs = fc[inc]
+                groups = {}
+                for k, v in zip(keys.tolist(), costs.tolist()):
+                    groups.setdefault(k, []).append(v)
+                best_k = min(sorted(groups), key=lambda k: sum(groups[k]) / len(groups[k]))
+                nearest = next((r for r in sel if str(r) == str(best_k)), sel[0])
+        out[ids_str == ex_s] = nearest
+    return out

@@ -16,6 +16,14 @@ pytestmark = pytest.mark.gpu
 REW_ATOL = 1e-6
 
 
+@pytest.fixture(params=["lane", "group"])
+def alloc_impl(request, monkeypatch):
+    # both phase-B allocation kernels (one env per lane / one env per lane group) against the same
+    # references; msc_env_create picks by shape otherwise (small test batches would get the group one)
+    monkeypatch.setenv("MSC_ALLOC_IMPL", request.param)
+    return request.param
+
+
 def _vec(spec, E, **kw):
     from marlsc.vec_env import VecInventoryEnv
     return VecInventoryEnv(None, E, spec=spec, device=0, **kw)
@@ -26,6 +34,7 @@ def _np(t):
 
 
 @pytest.mark.parametrize("name", ENV_FIXTURES)
+@pytest.mark.usefixtures("alloc_impl")
 def test_gpu_matches_reference_golden(name):
     d, meta = load(name)
     spec = spec_of(d, meta)
@@ -86,6 +95,7 @@ def _lockstep(spec, E, steps, seed=0, base_seed=777, check_every=1):
     return env, ref
 
 
+@pytest.mark.usefixtures("alloc_impl")
 def test_bench_config_vs_oracle_across_episode_boundary():
     # BASELINE configs 2-4 shape (8 x 64 x 5), 512 envs, 110 steps (one in-kernel auto-reset)
     cfg = make_synthetic_env_config(8, 64, 5)
@@ -93,6 +103,7 @@ def test_bench_config_vs_oracle_across_episode_boundary():
     _lockstep(spec, 512, 110, check_every=10)
 
 
+@pytest.mark.usefixtures("alloc_impl")
 def test_c5_shape_vs_oracle():
     cfg = make_synthetic_env_config(16, 256, 5, episode_length=12)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
@@ -100,6 +111,7 @@ def test_c5_shape_vs_oracle():
 
 
 @pytest.mark.parametrize("name", ["c8_split", "variant_a", "variant_b", "variant_c", "repo_3wh5sku"])
+@pytest.mark.usefixtures("alloc_impl")
 def test_variants_vs_oracle_many_envs(name):
     d, meta = load(name)
     _lockstep(spec_of(d, meta), 300, 70, seed=3, check_every=7)
@@ -338,6 +350,7 @@ def test_launch_timing_counts_and_results_unchanged():
                                              # limit: long units, many carried products
     (16, 9, 4, 6.0, 0.5, 7.5, "shipment"),   # widest group (16 warehouses per env)
 ])
+@pytest.mark.usefixtures("alloc_impl")
 def test_demand_and_allocation_edges_vs_oracle(W, R, K, lo, p, lq, lost):
     cfg = make_synthetic_env_config(W, R, K, episode_length=15, lambda_orders=lo, probability_skus=p,
                                     lambda_quantity=lq, lost_sales=lost)
@@ -346,6 +359,7 @@ def test_demand_and_allocation_edges_vs_oracle(W, R, K, lo, p, lq, lost):
 
 
 @pytest.mark.parametrize("lost", ["shipment", "closest"])
+@pytest.mark.usefixtures("alloc_impl")
 def test_shared_home_regions_vs_oracle(lost):
     # n_regions < n_warehouses: several warehouses share a home region (multi_env.py:144), which
     # takes the allocation kernel's LDS shipped-home path; home-region features are observed
@@ -365,6 +379,7 @@ def test_home_features_and_group_allocator_agree():
                  units_shipped_away=True, stockout=True)
     cfg = make_synthetic_env_config(8, 64, 5, episode_length=30, features=feats)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    os.environ["MSC_ALLOC_IMPL"] = "lane"
     _lockstep(spec, 128, 12, seed=9, check_every=3)
     os.environ["MSC_ALLOC_IMPL"] = "group"
     try:
@@ -403,3 +418,18 @@ def test_gae_vectorised_equals_scalar():
             os.environ.pop("MSC_GAE_SCALAR", None)
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     np.testing.assert_allclose(_np(outs[0][2]), _np(outs[1][2]), rtol=1e-12)
+
+
+@pytest.mark.parametrize("W,R,lost", [(16, 256, "shipment"), (3, 5, "cost")])
+@pytest.mark.usefixtures("alloc_impl")
+def test_empirical_trace_demand_vs_oracle(W, R, lost):
+    # EmpiricalDemandSampler (demand_sampler.py:214-261): per-episode window start drawn from the
+    # demand stream, one trace timestep per step from the CSR trace, across two episode
+    # boundaries; BASELINE configs[4] shape (16 x 256 x 5) with ~200-1,000 orders per step.
+    # Pinned to the C oracle's restatement (no reference fixture covers this sampler: SURVEY 8(c)).
+    from marlsc.synthetic import make_synthetic_trace
+    cfg = make_synthetic_env_config(W, R, 5, episode_length=6, lost_sales=lost)
+    cfg["components"]["demand_sampler"] = {"type": "empirical", "params": None}
+    trace = make_synthetic_trace(R, 5, 25, orders_per_step=(200, 1000) if R > 64 else (2, 12), seed=W)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True, "demand_trace": trace})
+    _lockstep(spec, 96, 14, seed=4, check_every=3)

@@ -68,8 +68,13 @@ int main() {
       Pcg64 b = a; uint64_t th = a.s_hi, tl = a.s_lo;
       for (int k = 0; k < 20; k++) {
         for (int j = 0; j < G; j++) pcg_step(b);
-        uint64_t nh, nl; mul128(th, tl, mh, ml, nh, nl); add128(nh, nl, ch, cl); th = nh; tl = nl;
-        if (th != b.s_hi || tl != b.s_lo) { printf("jump G=%d\n", G); return 1; }
+        uint64_t nh, nl; mul128(th, tl, mh, ml, nh, nl); add128(nh, nl, ch, cl);
+        uint64_t qh = th, ql = tl; lcg128(qh, ql, mh, ml, ch, cl);  // the generators' form
+        th = nh; tl = nl;
+        if (th != b.s_hi || tl != b.s_lo || qh != th || ql != tl) { printf("jump G=%d\n", G); return 1; }
+        // the generators' double: bit-identical to numpy's random() of the same output
+        const double u1 = u64_to_double(pcg_output(th, tl)), u2 = pcg_output_double(th, tl);
+        if (u1 != u2) { printf("double %d\n", k); return 1; }
       }
     }
   }
@@ -212,3 +217,30 @@ def test_repo_config_files_load(name, dims):
     cfg = load_environment_config(str(REPO / "config_files" / "environments" / f"{name}.yaml"), allow_nr_ne_nw=True)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True}, allow_nr_ne_nw=True)
     assert (spec.W, spec.R, spec.K, spec.local_obs_dim) == dims
+
+
+def test_map_excluded_regions():
+    # DataProcessor.map_excluded_regions (preprocessor.py:382-441): an excluded region goes to the
+    # selected region that shares its warehouses with the lowest mean fixed cost (ties: smallest
+    # id), else to selected_region_ids[0]
+    from marlsc.trace import map_excluded_regions
+    w2r = {"sourcenodeid": ["W1", "W1", "W1", "W2", "W2", "W3", "W3"],
+           "destinationregionid": ["R9", "R1", "R2", "R9", "R2", "R7", "R3"],
+           "fixed_costs": [5.0, 4.0, 3.0, 1.0, 5.0, 2.0, 1.0]}
+    sel = ["R1", "R2", "R3"]
+    orders = np.array(["R1", "R9", "R2", "R8", "R9", "R7", "R3"], dtype=object)
+    got = map_excluded_regions(orders, sel, w2r)
+    # R9: warehouses {W1, W2}; selected pairs R1 (4), R2 (3, 5 -> mean 4) -> tie at 4 -> R1
+    # R8: no pairs -> R1; R7: warehouse W3 -> selected pair R3 (1) -> R3
+    assert got.tolist() == ["R1", "R1", "R2", "R1", "R1", "R3", "R3"]
+
+
+def test_synthetic_trace_packs_like_the_preprocessor_frame():
+    from marlsc.synthetic import make_synthetic_trace
+    from marlsc.trace import pack_demand_trace
+    tr = make_synthetic_trace(32, 5, 20, orders_per_step=(10, 40), seed=2)
+    n_orders = len(np.unique(tr["order_id"]))
+    p = pack_demand_trace(tr, 5)
+    assert p["n_rows"] == 20 and p["offsets"][-1] == n_orders
+    assert int(p["quantities"].sum()) == int(tr["quantity"].sum())  # every line has a SKU in [0, 5)
+    assert np.all(np.diff(p["regions"][p["offsets"][3]:p["offsets"][4]]) >= 0)  # region-major within a step
