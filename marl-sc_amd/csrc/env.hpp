@@ -37,6 +37,7 @@ struct EnvConst {
   int32_t shared_home;  // 1: some region is the home region of two or more warehouses
   int32_t demand_uni;   // 1: Poisson parameters equal across regions (demand_unit_kernel<UNI>)
   int32_t alloc_impl;   // phase B: 0 = one env per lane (alloc_lane_kernel); 1 = one env per lane group (step_b_kernel)
+  int32_t alloc_lpe;    // alloc_lane_kernel lanes per env forced by MSC_ALLOC_LPE (1, 2, 4); 0 = by env count
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;

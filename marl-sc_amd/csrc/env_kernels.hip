@@ -1022,22 +1022,7 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __
 }
 
 // ---- phase B ------------------------------------------------------------------------------
-// Butterfly partner exchange inside a group of GW lanes with DPP (a VALU operand modifier, no LDS
-// round trip): step 0 pairs lanes i ^ 1 and step 1 lanes i ^ 2 (quad_perm), step 2 the two quads
-// of an 8-lane row half (row_half_mirror), step 3 the two halves of a 16-lane row (row_mirror).
-// Every step pairs lanes whose partial results cover disjoint halves, so min / sum reductions end
-// with the group result in every lane.
-template <int S>
-__device__ __forceinline__ int dpp_x(int v) {
-  constexpr int ctrl = S == 0 ? 0xB1 : S == 1 ? 0x4E : S == 2 ? 0x141 : 0x140;
-  return __builtin_amdgcn_update_dpp(0, v, ctrl, 0xF, 0xF, false);
-}
-template <int S>
-__device__ __forceinline__ double dpp_x(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = dpp_x<S>((int)(b & 0xffffffffLL)), hi = dpp_x<S>((int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
+// (dpp_x: kcommon.hpp)
 template <int GW, typename T, typename F>
 __device__ __forceinline__ T group_reduce(T v, F op) {
   v = op(v, dpp_x<0>(v));

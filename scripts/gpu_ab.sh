@@ -10,8 +10,8 @@ if [ "${RUN_TESTS:-1}" = 1 ]; then
 fi
 for v in ${VARIANTS:-default=}; do
   name=${v%%=*}; assigns=${v#*=}
-  ( IFS=,; for a in $assigns; do [ -n "$a" ] && export "$a"; done
-    timeout -k 10 ${T_BENCH:-300} python bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline --rollout-T ${ROLLOUT_T:-100} > gpurun_out/ab_$name.log 2>&1 )
+  ( IFS=,; for a in $assigns; do [ -n "$a" ] && export "$a"; done; unset IFS
+    timeout -k 10 ${T_BENCH:-300} python bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline --rollout-T ${ROLLOUT_T:-100} ${BENCH_ARGS:-} > gpurun_out/ab_$name.log 2>&1 )
   rc=$?; echo "== $name rc=$rc"; grep -o '"ms_per_step[^,]*\|"kernels_ms": {[^}]*}' gpurun_out/ab_$name.log | tr '\n' ' '; echo
   [ $rc -eq 0 ] || exit $rc
 done

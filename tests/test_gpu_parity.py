@@ -24,6 +24,15 @@ def alloc_impl(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=["lane", "lane1", "lane2", "group"])
+def alloc_impl_lpe(request, monkeypatch):
+    # as alloc_impl, plus the lane kernel's 1 / 2 lanes-per-env forms (the small test batches get 4
+    # lanes per env by shape when there are >= 8 warehouses)
+    monkeypatch.setenv("MSC_ALLOC_IMPL", request.param[:4] if request.param != "group" else "group")
+    monkeypatch.setenv("MSC_ALLOC_LPE", request.param[4:] or "0")
+    return request.param
+
+
 def _vec(spec, E, **kw):
     from marlsc.vec_env import VecInventoryEnv
     return VecInventoryEnv(None, E, spec=spec, device=0, **kw)
@@ -95,7 +104,7 @@ def _lockstep(spec, E, steps, seed=0, base_seed=777, check_every=1):
     return env, ref
 
 
-@pytest.mark.usefixtures("alloc_impl")
+@pytest.mark.usefixtures("alloc_impl_lpe")
 def test_bench_config_vs_oracle_across_episode_boundary():
     # BASELINE configs 2-4 shape (8 x 64 x 5), 512 envs, 110 steps (one in-kernel auto-reset)
     cfg = make_synthetic_env_config(8, 64, 5)
@@ -103,7 +112,7 @@ def test_bench_config_vs_oracle_across_episode_boundary():
     _lockstep(spec, 512, 110, check_every=10)
 
 
-@pytest.mark.usefixtures("alloc_impl")
+@pytest.mark.usefixtures("alloc_impl_lpe")
 def test_c5_shape_vs_oracle():
     cfg = make_synthetic_env_config(16, 256, 5, episode_length=12)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
@@ -349,8 +358,9 @@ def test_launch_timing_counts_and_results_unchanged():
                                              # round) and rates near the multiplication method's
                                              # limit: long units, many carried products
     (16, 9, 4, 6.0, 0.5, 7.5, "shipment"),   # widest group (16 warehouses per env)
+    (12, 7, 3, 4.0, 0.6, 5.0, "closest"),    # masked warehouse slots (12 of 16; 3 of 4 per lane)
 ])
-@pytest.mark.usefixtures("alloc_impl")
+@pytest.mark.usefixtures("alloc_impl_lpe")
 def test_demand_and_allocation_edges_vs_oracle(W, R, K, lo, p, lq, lost):
     cfg = make_synthetic_env_config(W, R, K, episode_length=15, lambda_orders=lo, probability_skus=p,
                                     lambda_quantity=lq, lost_sales=lost)
@@ -421,7 +431,7 @@ def test_gae_vectorised_equals_scalar():
 
 
 @pytest.mark.parametrize("W,R,lost", [(16, 256, "shipment"), (3, 5, "cost")])
-@pytest.mark.usefixtures("alloc_impl")
+@pytest.mark.usefixtures("alloc_impl_lpe")
 def test_empirical_trace_demand_vs_oracle(W, R, lost):
     # EmpiricalDemandSampler (demand_sampler.py:214-261): per-episode window start drawn from the
     # demand stream, one trace timestep per step from the CSR trace, across two episode
