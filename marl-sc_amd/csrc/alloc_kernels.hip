@@ -53,7 +53,7 @@ struct AlLds {
     o = (o + 3) & ~3;
     L.out = o; o += MWL * 64 * 2;   // [i][lane] outbound cost (f64)
     L.pen = o; o += MWL * 64 * 2;   // [i][lane] penalty cost (f64)
-    L.tab = o; o += tab ? R * MW * 4 : 0;  // [r][w] {of, ov} (f64 pairs)
+    L.tab = o; o += tab ? (R | 1) * MW * 4 : 0;  // [w][r] {of, ov} (f64 pairs), row stride R | 1
     L.hm = o;  o += R;             // [r] home mask
     L.cl = o;  o += R;             // [r] closest warehouse
     L.total = o;
@@ -101,14 +101,19 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
   // read through `s` would be re-loaded after every store)
   MSC_GLOBAL int32_t* const incp = gp(s.inc);
   const double2* Ltab = TAB ? reinterpret_cast<const double2*>(al_lds + L.tab) : nullptr;
+  // table rows are warehouse-major with an odd stride (in 16-byte entries): the lanes' regions differ,
+  // and with [r][w] rows (a 128-byte stride at MW 8) every even region falls on the same banks (up to
+  // 8-way conflicts per 16-lane phase of the ds_read_b128); [w][r] puts consecutive regions on
+  // consecutive banks, and the odd stride spreads the warehouses of one region (LPE > 1)
+  const int RS = R | 1;
   const uint32_t* Lhm = reinterpret_cast<const uint32_t*>(al_lds + L.hm);
   const int32_t* Lcl = al_lds + L.cl;
   {
     double2* tw_ = reinterpret_cast<double2*>(al_lds + L.tab);
     if constexpr (TAB) {
       for (int i = lane; i < R * MW; i += 64) {
-        const int r = i / MW, w = i % MW;
-        tw_[i] = w < W ? make_double2(c.ofT[r * W + w], c.ovT[r * W + w]) : make_double2(0.0, 0.0);
+        const int w = i / R, r = i % R;
+        tw_[w * RS + r] = w < W ? make_double2(c.ofT[r * W + w], c.ovT[r * W + w]) : make_double2(0.0, 0.0);
       }
     }
     uint32_t* hm_ = reinterpret_cast<uint32_t*>(al_lds + L.hm);
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
     }
   }
   auto tab_at = [&](int r, int w) -> double2 {
-    if constexpr (TAB) return Ltab[r * MW + w];
+    if constexpr (TAB) return Ltab[w * RS + r];
     else return make_double2(gp(c.ofT)[r * W + w], gp(c.ovT)[r * W + w]);
   };
 
@@ -480,7 +485,7 @@ static size_t alloc_lane_lds_bytes(const EnvConst& c, int MW, int LPE, bool tab)
 // (no demand kernel beside this one) and at most one block per CU -- up to what the CU holds
 // (C5, 16 x 256: 64 KiB of table; read from L2 instead, its latency sits on every order's chain)
 static bool alloc_tab_in_lds(const EnvConst& c, int MW, int LPE) {
-  if ((size_t)c.R * MW * 16 <= AL_TAB_MAX) return true;
+  if ((size_t)(c.R | 1) * MW * 16 <= AL_TAB_MAX) return true;
   const int64_t blocks = (c.E * LPE + 63) / 64;
   return c.demand_type == MSC_DEMAND_EMPIRICAL && blocks <= 256 &&
          alloc_lane_lds_bytes(c, MW, LPE, true) <= 160 * 1024;
