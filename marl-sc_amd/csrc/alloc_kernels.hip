@@ -502,11 +502,11 @@ static void alloc_launch(F f, const EnvConst& c, const DevEnv* d, const StepIO& 
   hipLaunchKernelGGL(f, dim3((unsigned)((c.E * lpe + 63) / 64)), dim3(64), lds, st, d, io);
 }
 
-// lanes per env: enough waves to cover the chip when there are few envs (one-env-per-lane waves:
-// E / 64; below ~2 per CU the allocation chain runs on half-empty CUs). Only the plain (non-debug,
-// unshared-home, shipment / closest lost-sales) allocation is instantiated with LPE > 1.
+// lanes per env: 1 unless MSC_ALLOC_LPE asks for 2 or 4 (measured slower at every BASELINE shape:
+// DESIGN.md §3). Only the plain (non-debug, unshared-home, shipment / closest lost-sales)
+// allocation is instantiated with LPE > 1.
 static int alloc_lpe(const EnvConst& c, bool dbg, int MW) {
-  int lpe = c.alloc_lpe != 0 ? c.alloc_lpe : c.E >= 32768 ? 1 : c.E >= 16384 ? 2 : 4;
+  int lpe = c.alloc_lpe;
   if (lpe != 2 && lpe != 4) lpe = 1;
   if (dbg || shared_homes(c) || c.lost_type == MSC_LOST_COST || MW < 8) lpe = 1;
   return lpe;

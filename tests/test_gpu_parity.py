@@ -24,10 +24,9 @@ def alloc_impl(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lane", "lane1", "lane2", "group"])
+@pytest.fixture(params=["lane", "lane2", "lane4", "group"])
 def alloc_impl_lpe(request, monkeypatch):
-    # as alloc_impl, plus the lane kernel's 1 / 2 lanes-per-env forms (the small test batches get 4
-    # lanes per env by shape when there are >= 8 warehouses)
+    # as alloc_impl, plus the lane kernel's 2 / 4 lanes-per-env forms (A/B; >= 8 warehouses)
     monkeypatch.setenv("MSC_ALLOC_IMPL", request.param[:4] if request.param != "group" else "group")
     monkeypatch.setenv("MSC_ALLOC_LPE", request.param[4:] or "0")
     return request.param
