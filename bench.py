@@ -34,6 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
 # v_add_u32 at 4 waves per SIMD retire one wave64 instruction per 1.78 ns per SIMD, i.e.
 # 1024 SIMDs / 1.784 ns = 574 G wave-instructions/s (integer multiplies and f64 mul/compare: 430-500)
 VALU_PEAK_WINST = 1024 / 1.784e-9
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
 DEMAND_KERNEL = "demand_unit_kernel"
 STEP_KERNELS = ("step_a_kernel", "alloc_lane_kernel", "step_c_kernel")
 GAE_BYTES_PER_ELEM = 4 + 4 + 1 + 1 + 4 + 4  # reward, value, terminated, truncated in; advantage, target out (next value: truncated rows only)
@@ -114,6 +115,9 @@ def main():
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "traffic.json"))
     ap.add_argument("--rollout-T", type=int, default=100,
                     help="steps of the MAPPO rollout line (0 = skip): env + actor/critic forward + buffers + GAE")
+    ap.add_argument("--rollout-lanes", type=int, default=int(os.environ.get("MSC_ROLLOUT_LANES", "1")),
+                    help="env handles the rollout's envs are split into, each stepping on its own HIP stream so one "
+                         "lane's env kernels overlap another's policy GEMMs (1 = one handle, one stream)")
     args = ap.parse_args()
 
     import torch
@@ -191,8 +195,18 @@ def main():
         rc = RolloutConfig.from_algorithm_config(yaml.safe_load(open(REPO / "config_files/algorithms/mappo.yaml")))
         torch.manual_seed(0)
         module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
-        col = RolloutCollector(env, module, args.rollout_T, seed=rank)
-        env.set_pipelining(True)
+        nl = max(1, args.rollout_lanes)
+        if nl == 1:
+            renv = env
+            env.set_pipelining(True)
+        else:  # the rank's envs (same global ids) as nl handles of consecutive env-id ranges
+            cuts = [E * j // nl for j in range(nl + 1)]
+            renv = [VecInventoryEnv(None, cuts[j + 1] - cuts[j], spec=spec, device=dev, base_seed=default_train_seed(42),
+                                    env_index_offset=rank * E + cuts[j]) for j in range(nl)]
+            for x in renv:
+                x.set_pipelining(os.environ.get("MSC_ROLLOUT_PIPELINE", "1") != "0")
+                x.reset()
+        col = RolloutCollector(renv, module, args.rollout_T, seed=rank)
         col.collect()  # warm-up (GEMM heuristics, allocator)
         if world > 1:
             dist.barrier()
@@ -203,7 +217,8 @@ def main():
         if world > 1:
             dist.barrier()
         t_roll = time.perf_counter() - t0
-        env.check()
+        for x in (renv if isinstance(renv, list) else [renv]):
+            x.check()
     # (4) the HBM-bound kernel of the rollout: msc_gae (GAE reverse scan + advantage statistics) over
     #     one MAPPO rollout's [T, E * W] sequences, timed alone with events on its stream
     gae_line = None
@@ -235,6 +250,35 @@ def main():
                     "bytes_per_launch": int(gb), "ms": round(t_gae * 1e3, 4),
                     "shape": f"T={T} x N={N} sequences (E x W of one MAPPO rollout), {GAE_BYTES_PER_ELEM} B/element"}
         del r_, v_, nv_, te_, tr_, adv_, tgt_
+    # (5) the MFMA-bound kernel of the rollout: the fused actor MLP (msc_mlp3_relu_forward) over one
+    #     step's E * W rows, timed alone with events on its stream
+    mlp_line = None
+    if rank == 0 and args.rollout_T > 0:
+        from marlsc.mlp import fusable, mlp3_forward
+        mods = list(module.actor)
+        if fusable(mods):
+            N = E * spec.W
+            xg = torch.randn((N, spec.local_obs_dim), device="cuda", generator=torch.Generator(device="cuda").manual_seed(8))
+            yo = torch.empty((N, spec.K), device="cuda")
+            with torch.no_grad():
+                for _ in range(3):
+                    mlp3_forward(mods, xg, out=yo)
+                reps = 20
+                ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ea.record()
+                for _ in range(reps):
+                    mlp3_forward(mods, xg, out=yo)
+                eb.record()
+                torch.cuda.synchronize()
+            t_mlp = ea.elapsed_time(eb) / 1e3 / reps
+            H1, H2 = mods[0].out_features, mods[2].out_features
+            fl = 2.0 * N * (spec.local_obs_dim * H1 + H1 * H2 + H2 * spec.K)
+            mlp_line = {"kernel": "mlp3_relu_kernel", "bound": "mfma", "achieved": round(fl / t_mlp / 1e12, 2),
+                        "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(fl / t_mlp / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
+                        "flops_per_launch": int(fl), "ms": round(t_mlp * 1e3, 4),
+                        "shape": f"actor {spec.local_obs_dim}-{H1}-{H2}-{spec.K} over N={N} rows (E x W of one rollout step), "
+                                 f"f32 MFMA, timed alone"}
+            del xg, yo
     tt = torch.tensor([dt, t_roll], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -311,13 +355,16 @@ def main():
             out["roofline"]["step_valu_issue"] = step_valu
         if gae_line is not None:
             out["roofline_gae"] = gae_line
+        if mlp_line is not None:
+            out["roofline_mlp"] = mlp_line
         if args.rollout_T > 0:
             out["rollout"] = {
                 "value": round(E * world * spec.W * args.rollout_T / t_roll, 1), "unit": "agent-steps/s",
                 "ms_per_step": round(t_roll / args.rollout_T * 1e3, 4), "T": args.rollout_T,
-                "policy": f"MAPPO (config_files/algorithms/mappo.yaml): actor {spec.local_obs_dim}-256-256-{spec.K}, "
+                "policy": f"MAPPO (config_files/algorithms/mappo.yaml): actor {spec.local_obs_dim}-256-256-{spec.K} (fused f32-MFMA kernel), "
                           f"critic {spec.local_obs_dim * (1 + spec.W)}-64-64-1, fp32, parameter sharing",
-                "includes": "env step, actor forward, MAPPO critic on local||global (first layer split: global block once per env), Gaussian sampling, "
+                "lanes": max(1, args.rollout_lanes),
+                "includes": "env step (envs split into `lanes` handles on their own HIP streams), actor forward, MAPPO critic on local||global (first layer split: global block once per env), Gaussian sampling, "
                             "buffer writes, truncation bootstrap, GAE kernel, adv-norm all-reduce + normalise"}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)

@@ -272,6 +272,19 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
                         const float* eps, int64_t n_rows, int32_t k, float* actions, float* logp,
                         float* clipped, msc_stream_t stream);
 
+/* Rollout policy inference (replaces the actor's torch layer sequence in the EnvRunner's
+ * _forward_inference, rlmodules/base.py:480-557, for MLPArchitecture.build networks,
+ * architectures/mlp.py:14-60): out = W3 relu(W2 relu(W1 x + b1) + b2) + b3 for n_rows rows of
+ * in_dim floats, in one kernel on the f32 MFMA (hidden activations stay in registers).
+ * hidden1 == hidden2 in {64, 128, 256}; out_dim <= 32. Weights are passed in the packed fragment
+ * order the kernel streams (marlsc/mlp.py:pack_mlp3 builds them from the torch [out, in] matrices):
+ *   w1p [hidden1/32][ceil(in_dim/2)][64], w2p [hidden2/32][hidden1/8][64][4], w3p [hidden2/8][64][4];
+ * biases b1 [hidden1], b2 [hidden2], b3 [out_dim] as in torch. x [n_rows][in_dim], out [n_rows][out_dim]:
+ * f32 device buffers; stream-ordered. */
+int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
+                          int32_t out_dim, const float* w1p, const float* b1, const float* w2p, const float* b2,
+                          const float* w3p, const float* b3, float* out, msc_stream_t stream);
+
 /* Utility: SeedSequence(words).generate_state(1, uint32)[0] (numpy-compatible), on the host. */
 uint32_t msc_seedseq_u32(const uint32_t* words, int32_t n_words);
 

@@ -1,0 +1,128 @@
+"""Fused policy-MLP inference for the rollout (msc_mlp3_relu_forward, csrc/mlp.hip).
+
+The reference's actor / critic networks are `MLPArchitecture.build` MLPs
+(src/algorithms/models/architectures/mlp.py:14-60): Linear -> ReLU per hidden size, then an output
+Linear. At rollout (inference, no autograd) a two-hidden-layer ReLU MLP with equal hidden sizes of
+64, 128 or 256 -- both actors and the IPPO critic of config_files/algorithms/{ippo,mappo}.yaml --
+runs as ONE HIP kernel on the f32 MFMA with the hidden activations in registers. The kernel
+streams the weights in a lane-major fragment order; `pack_mlp3` builds it from the torch [out, in]
+matrices (index maps cached per shape, packs cached per weight version, so the learner's updates
+are picked up and the pack is rebuilt at most once per optimizer step).
+
+There is no CPU fallback: a CUDA tensor on a build without libmarlsc raises (abi.lib()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import abi
+
+HIDDEN_SIZES = (64, 128, 256)
+MAX_OUT = 32
+ENABLED = os.environ.get("MSC_FUSED_MLP3", "1") != "0"
+
+_IDX: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
+
+
+def _rho(r: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """Row of register r in lane half h of a 32x32 f32 MFMA accumulator."""
+    return (r & 3) + 8 * (r >> 2) + 4 * h
+
+
+def _index_maps(L: int, H1: int, H2: int, KO: int, device) -> Tuple[torch.Tensor, ...]:
+    key = (L, H1, H2, KO, str(device))
+    if key in _IDX:
+        return _IDX[key]
+    KS1 = (L + 1) // 2
+    lane = torch.arange(64, device=device)
+    c, h = lane & 31, lane >> 5
+    # w1p[t][m][lane] = W1[32 t + c][h KS1 + m]  (0 past in_dim)
+    t = torch.arange(H1 // 32, device=device)[:, None, None]
+    m = torch.arange(KS1, device=device)[None, :, None]
+    f = h * KS1 + m
+    i1 = ((t * 32 + c) * L + f.clamp(max=L - 1)).reshape(-1)
+    v1 = (f < L).expand(H1 // 32, KS1, 64).reshape(-1)
+    # w2p[t2][s4][lane][i] = W2[32 t2 + c][32 t1 + rho(r, h)], s = 4 s4 + i = 16 t1 + r
+    S = (H1 // 32) * 16
+    t2 = torch.arange(H2 // 32, device=device)[:, None, None, None]
+    s = (torch.arange(S // 4, device=device)[None, :, None, None] * 4 + torch.arange(4, device=device)[None, None, None, :])
+    hh = h[None, None, :, None]
+    cc = c[None, None, :, None]
+    i2 = ((t2 * 32 + cc) * H1 + (s // 16) * 32 + _rho(s % 16, hh)).reshape(-1)
+    # w3p[q][lane][i] = W3[c][32 (q // 4) + rho(4 (q % 4) + i, h)]  (0 for output rows >= KO)
+    q = torch.arange((H2 // 32) * 4, device=device)[:, None, None]
+    r = (q % 4) * 4 + torch.arange(4, device=device)[None, None, :]
+    c3, h3 = c[None, :, None], h[None, :, None]
+    i3 = (c3.clamp(max=KO - 1) * H2 + (q // 4) * 32 + _rho(r, h3)).reshape(-1)
+    v3 = (c3 < KO).expand((H2 // 32) * 4, 64, 4).reshape(-1)
+    _IDX[key] = (i1, v1, i2, i3, v3)
+    return _IDX[key]
+
+
+def pack_mlp3(w1: torch.Tensor, w2: torch.Tensor, w3: torch.Tensor):
+    """Torch Linear weights ([H1, L], [H2, H1], [KO, H2]) -> (w1p, w2p, w3p) fragment order."""
+    H1, L = w1.shape
+    H2, KO = w2.shape[0], w3.shape[0]
+    i1, v1, i2, i3, v3 = _index_maps(L, H1, H2, KO, w1.device)
+    zero = torch.zeros((), device=w1.device, dtype=torch.float32)
+    w1p = torch.where(v1, w1.detach().float().reshape(-1)[i1], zero)
+    w2p = w2.detach().float().reshape(-1)[i2]
+    w3p = torch.where(v3, w3.detach().float().reshape(-1)[i3], zero)
+    return w1p.contiguous(), w2p.contiguous(), w3p.contiguous()
+
+
+def fusable(mods) -> bool:
+    """Linear, ReLU, Linear, ReLU, Linear with equal supported hidden sizes and <= 32 outputs."""
+    if len(mods) != 5:
+        return False
+    l1, a1, l2, a2, l3 = mods
+    if not (isinstance(l1, nn.Linear) and isinstance(l2, nn.Linear) and isinstance(l3, nn.Linear)
+            and isinstance(a1, nn.ReLU) and isinstance(a2, nn.ReLU)):
+        return False
+    if l1.bias is None or l2.bias is None or l3.bias is None:
+        return False
+    H1, H2 = l1.out_features, l2.out_features
+    return H1 == H2 and H1 in HIDDEN_SIZES and l2.in_features == H1 and l3.in_features == H2 and l3.out_features <= MAX_OUT
+
+
+class _Pack:
+    __slots__ = ("key", "tensors")
+
+    def __init__(self):
+        self.key, self.tensors = None, None
+
+
+def mlp3_forward(mods, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The fused kernel over x [..., L] (f32 CUDA) -> [..., KO]; mods as accepted by fusable()."""
+    l1, _, l2, _, l3 = mods
+    L, KO = l1.in_features, l3.out_features
+    if x.shape[-1] != L:
+        raise ValueError(f"input has {x.shape[-1]} features, the MLP expects {L}")
+    # pack cache on the first Linear: rebuilt when any weight changes (version counters) or moves
+    pk = getattr(l1, "_msc_pack", None)
+    if pk is None:
+        pk = _Pack()
+        l1._msc_pack = pk
+    key = tuple((p.data_ptr(), p._version) for p in (l1.weight, l2.weight, l3.weight))
+    if pk.key != key:
+        pk.tensors = pack_mlp3(l1.weight, l2.weight, l3.weight)
+        pk.key = key
+    w1p, w2p, w3p = pk.tensors
+    lead = x.shape[:-1]
+    xf = x.reshape(-1, L)
+    if xf.dtype != torch.float32 or not xf.is_contiguous():
+        xf = xf.float().contiguous()
+    n = xf.shape[0]
+    if out is None:
+        out = torch.empty((n, KO), device=x.device, dtype=torch.float32)
+    b1, b2, b3 = (m.bias.detach().float().contiguous() for m in (l1, l2, l3))
+    vp = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    abi.check(abi.lib().msc_mlp3_relu_forward(vp(xf), n, L, l1.out_features, l2.out_features, KO, vp(w1p), vp(b1),
+                                              vp(w2p), vp(b2), vp(w3p), vp(b3), vp(out),
+                                              C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    return out.reshape(*lead, KO)

@@ -18,6 +18,7 @@ at C3); the MAPPO critic's flat input (local || global of the same env) is rebui
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 from dataclasses import dataclass
@@ -27,7 +28,9 @@ import torch
 import torch.nn as nn
 
 from . import abi
+from . import mlp as mlp3
 from .dist import allreduce_adv_stats
+from .mlp import mlp3_forward
 from .vec_env import VecInventoryEnv
 
 _ACT = {"relu": nn.ReLU, "tanh": nn.Tanh, "elu": nn.ELU, "gelu": nn.GELU, "sigmoid": nn.Sigmoid}
@@ -52,9 +55,10 @@ class MLP(nn.Sequential):
         return mlp_forward(self, x)
 
 
-# Inference (no autograd) runs each Linear -> ReLU pair as one GEMM with the ReLU in the GEMM
-# epilogue (torch._addmm_activation -> hipBLASLt), instead of a GEMM plus a separate elementwise
-# pass over the [N, hidden] activations. MSC_FUSED_MLP=0 restores the plain layer sequence.
+# Inference (no autograd): a whole Linear-ReLU-Linear-ReLU-Linear MLP with hidden sizes 64 / 128 /
+# 256 (both actors, the IPPO critic) runs as one f32-MFMA kernel (marlsc/mlp.py, MSC_FUSED_MLP3=0
+# turns it off); any other Linear -> ReLU pair runs as one GEMM with the ReLU in the GEMM epilogue
+# (torch._addmm_activation -> hipBLASLt). MSC_FUSED_MLP=0 restores the plain layer sequence.
 _FUSED = os.environ.get("MSC_FUSED_MLP", "1") != "0"
 
 
@@ -65,6 +69,8 @@ def mlp_forward(layers, x: torch.Tensor, start: int = 0) -> torch.Tensor:
         for m in mods:
             x = m(x)
         return x
+    if mlp3.ENABLED and x.dtype == torch.float32 and mlp3.fusable(mods):
+        return mlp3_forward(mods, x)  # the whole MLP as one f32-MFMA kernel (csrc/mlp.hip)
     i = 0
     while i < len(mods):
         m = mods[i]
@@ -208,17 +214,40 @@ def normalize_advantages(adv: torch.Tensor, stats: torch.Tensor) -> torch.Tensor
     return adv
 
 
+class _Lane:
+    """One env handle of a collector: its slice [e0, e1) of the buffers' env axis and the HIP stream
+    its step chain (policy forward -> sampling -> env step) is issued on (None: the caller's)."""
+
+    def __init__(self, env: VecInventoryEnv, e0: int, stream: Optional[torch.cuda.Stream], flat: Optional[torch.Tensor]):
+        self.env, self.e0, self.e1, self.stream, self.flat = env, e0, e0 + env.n_envs, stream, flat
+        self.obs: Optional[torch.Tensor] = None
+
+    def ctx(self):
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+
 class RolloutCollector:
     """T steps of E envs x W agents (N = E*W sequences). Advantages are standardised per module as
     RLlib's GAE connector does: over every agent for one shared policy (adv_groups = 1), per agent
-    for one policy per agent (adv_groups = W)."""
+    for one policy per agent (adv_groups = W).
 
-    def __init__(self, env: VecInventoryEnv, module: ActorCritic, T: int, *, seed: int = 0,
-                 adv_groups: int = 1):
-        self.env, self.module, self.T = env, module, int(T)
-        E, W, K, L = env.n_envs, env.W, env.K, env.local_obs_dim
-        dev = env.device
-        self.N = E * W
+    `env` may be a list of env handles (lanes) covering consecutive env-id ranges, e.g. the two
+    halves of a rank's envs: each lane's step chain runs on its own HIP stream, so one lane's env
+    kernels (VALU-bound) overlap the other lane's policy GEMMs (MFMA-bound). The buffers' env axis
+    is the concatenation of the lanes; each env's trajectory is the same as with one handle (envs
+    are independent and seeded by global id), the Gaussian noise differs (drawn per lane)."""
+
+    def __init__(self, env, module: ActorCritic, T: int, *, seed: int = 0, adv_groups: int = 1):
+        envs = list(env) if isinstance(env, (list, tuple)) else [env]
+        e0 = envs[0]
+        for x in envs[1:]:
+            if x.spec is not e0.spec and (x.W, x.K, x.L) != (e0.W, e0.K, e0.L):
+                raise ValueError("rollout lanes must share one env spec")
+        self.env, self.envs, self.module, self.T = e0, envs, module, int(T)
+        E = sum(x.n_envs for x in envs)
+        W, K, L = e0.W, e0.K, e0.local_obs_dim
+        dev = e0.device
+        self.E, self.N = E, E * W
         self.obs = torch.empty((T, E, W, L), device=dev)
         self.actions = torch.empty((T, E, W, K), device=dev)
         self.logp = torch.empty((T, E, W), device=dev)
@@ -233,39 +262,59 @@ class RolloutCollector:
             raise ValueError(f"adv_groups must be 1 (shared policy) or W={W} (one policy per agent)")
         self.adv_groups = int(adv_groups)
         self.stats = torch.zeros((self.adv_groups, 3), dtype=torch.float64, device=dev)
-        self._flat = torch.empty((E, W, L * (1 + W)), device=dev)
-        self._gen = torch.Generator(device=dev).manual_seed(seed)
         self._need_flat = module.rc.actor_obs_type == "global"  # the critic splits its first layer
+        self._gen = torch.Generator(device=dev).manual_seed(seed)
+        self._lanes, off = [], 0
+        for x in envs:
+            st = torch.cuda.Stream(device=dev) if len(envs) > 1 else None
+            flat = torch.empty((x.n_envs, W, L * (1 + W)), device=dev) if self._need_flat else None
+            self._lanes.append(_Lane(x, off, st, flat))
+            off += x.n_envs
 
-    def _full(self, obs):
-        return self.env.obs_flat(obs=obs, out=self._flat) if self._need_flat else None
+    def _full(self, ln: _Lane, obs):
+        return ln.env.obs_flat(obs=obs, out=ln.flat) if self._need_flat else None
+
+    def _step(self, ln: _Lane, t: int) -> None:
+        env, m, sl, obs = ln.env, self.module, slice(ln.e0, ln.e1), ln.obs
+        self.obs[t, sl].copy_(obs)
+        full = self._full(ln, obs)
+        mean, log_std = m.dist_inputs(obs, full)
+        self.values[t, sl] = m.values(obs, full)
+        eps = torch.randn(mean.shape, device=mean.device, generator=self._gen)
+        # sample, log-density and the env's clip in one HIP kernel (msc_gaussian_sample)
+        # log_std [E, W, K] is a broadcast of one row (shared policy) or of W rows (per agent)
+        a = gaussian_sample(mean.contiguous(), log_std[0], m.rc.logstd_floor, eps, self.actions[t, sl], self.logp[t, sl])
+        may_end = env.may_truncate()
+        ln.obs, rew, trunc, final_obs = env.step(a)
+        self.rewards[t, sl] = rew
+        self.truncated[t, sl] = trunc.unsqueeze(-1)
+        # truncation bootstrap: V(final_obs) for the envs whose episode ended at this step
+        # (skipped while the envs are known to be mid-episode in lockstep)
+        if may_end:
+            full_f = self._full(ln, final_obs)
+            self.next_values[t, sl] = torch.where(trunc.bool().unsqueeze(-1), m.values(final_obs, full_f),
+                                                  torch.zeros((), device=final_obs.device))
+        else:
+            self.next_values[t, sl].zero_()
 
     @torch.no_grad()
     def collect(self, normalize: bool = True) -> Dict[str, torch.Tensor]:
-        env, m, T = self.env, self.module, self.T
-        obs = env.obs
+        m, T = self.module, self.T
+        main = torch.cuda.current_stream()
+        for ln in self._lanes:
+            ln.obs = ln.env.obs
+            if ln.stream is not None:
+                ln.stream.wait_stream(main)
+        # lanes interleaved per step on the host; each lane's chain is ordered on its own stream
         for t in range(T):
-            self.obs[t].copy_(obs)
-            full = self._full(obs)
-            mean, log_std = m.dist_inputs(obs, full)
-            self.values[t] = m.values(obs, full)
-            eps = torch.randn(mean.shape, device=mean.device, generator=self._gen)
-            # sample, log-density and the env's clip in one HIP kernel (msc_gaussian_sample)
-            # log_std [E, W, K] is a broadcast of one row (shared policy) or of W rows (per agent)
-            a = gaussian_sample(mean.contiguous(), log_std[0], m.rc.logstd_floor, eps, self.actions[t], self.logp[t])
-            may_end = env.may_truncate()
-            obs, rew, trunc, final_obs = env.step(a)
-            self.rewards[t] = rew
-            self.truncated[t] = trunc.unsqueeze(-1)
-            # truncation bootstrap: V(final_obs) for the envs whose episode ended at this step
-            # (skipped while the envs are known to be mid-episode in lockstep)
-            if may_end:
-                full_f = self._full(final_obs)
-                self.next_values[t] = torch.where(trunc.bool().unsqueeze(-1), m.values(final_obs, full_f),
-                                                  torch.zeros((), device=obs.device))
-            else:
-                self.next_values[t].zero_()
-        self.values[T] = m.values(obs, self._full(obs))
+            for ln in self._lanes:
+                with ln.ctx():
+                    self._step(ln, t)
+        for ln in self._lanes:
+            with ln.ctx():
+                self.values[T, ln.e0:ln.e1] = m.values(ln.obs, self._full(ln, ln.obs))
+            if ln.stream is not None:
+                main.wait_stream(ln.stream)
         N = self.N
         gae(self.rewards.view(T, N), self.values.view(T + 1, N), self.next_values.view(T, N),
             self.terminated.view(T, N), self.truncated.view(T, N), m.rc.gamma, m.rc.lam,

@@ -68,6 +68,45 @@ def test_rollout_replays_bit_exact_on_a_fresh_env():
         assert torch.equal(rew, col.rewards[t])
 
 
+def test_two_lane_rollout_matches_one_env_per_lane():
+    # a collector over two env handles (consecutive global env ids, one HIP stream each) fills the
+    # buffers' env axis lane by lane: every env consumed exactly its sampled actions (replay on one
+    # fresh handle of all envs is bit-exact), the stored values are the critic on the stored
+    # observations, and GAE over the joined buffers equals the numpy restatement
+    from marlsc import make_synthetic_env_config
+    from marlsc.rollout import ActorCritic, RolloutCollector, RolloutConfig
+    from marlsc.spec import EnvSpec
+    from marlsc.vec_env import VecInventoryEnv
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=7)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    E, T = 192, 16
+    lanes = [VecInventoryEnv(None, 64, spec=spec, device=0, base_seed=77, env_index_offset=0),
+             VecInventoryEnv(None, E - 64, spec=spec, device=0, base_seed=77, env_index_offset=64)]
+    for x in lanes:
+        x.reset()
+    torch.manual_seed(0)
+    m = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, RolloutConfig()).cuda()
+    col = RolloutCollector(lanes, m, T, seed=3)
+    col.collect(normalize=False)
+    torch.cuda.synchronize()
+    env2 = VecInventoryEnv(None, E, spec=spec, device=0, base_seed=77)
+    obs = env2.reset()
+    for t in range(T):
+        assert torch.equal(obs, col.obs[t])
+        obs, rew, trunc, _ = env2.step(col.actions[t].clamp(-1.0, 1.0).contiguous())
+        assert torch.equal(rew, col.rewards[t])
+        assert torch.equal(trunc, col.truncated[t, :, 0])
+    N = col.N
+    r = col.rewards.view(T, N).double().cpu().numpy()
+    v = col.values.view(T + 1, N).double().cpu().numpy()
+    nv = col.next_values.view(T, N).double().cpu().numpy()
+    a_ref, _ = gae_np(r, v, nv, col.terminated.view(T, N).cpu().numpy(), col.truncated.view(T, N).cpu().numpy(), 0.99, 0.95)
+    np.testing.assert_allclose(col.adv.view(T, N).cpu().numpy(), a_ref, rtol=1e-4, atol=1e-4)
+    with torch.no_grad():
+        v5 = m.values(col.obs[5])
+    torch.testing.assert_close(v5, col.values[5], rtol=1e-5, atol=1e-5)
+
+
 def test_fused_linear_relu_inference_matches_layer_sequence():
     # rollout inference runs Linear -> ReLU pairs as one GEMM with a ReLU epilogue; the plain layer
     # sequence (autograd path, used by the learner) must agree to GEMM rounding
@@ -84,6 +123,30 @@ def test_fused_linear_relu_inference_matches_layer_sequence():
         pc = split_global_mlp(mlp, x)
     torch.testing.assert_close(fa, pa.detach(), rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(fc, pc.detach(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("L,H,KO,n", [(34, 256, 5, 262144 // 64), (42, 256, 5, 1000), (34, 64, 1, 77),
+                                       (306, 64, 1, 4096), (33, 128, 32, 31), (1, 256, 5, 64)])
+def test_fused_mlp3_kernel_matches_torch_layers(L, H, KO, n):
+    # msc_mlp3_relu_forward (one f32-MFMA kernel, hidden activations in registers) against the torch
+    # fp32 layer sequence of the same MLP: ragged row counts, odd input widths, 1..32 outputs
+    from marlsc.mlp import fusable, mlp3_forward
+    from marlsc.rollout import MLP
+    torch.manual_seed(L + H + KO)
+    mlp = MLP(L, KO, {"hidden_sizes": [H, H]}).cuda()
+    mods = list(mlp)
+    assert fusable(mods)
+    x = torch.randn(n, L, device="cuda")
+    with torch.no_grad():
+        ref = mods[4](torch.relu(mods[2](torch.relu(mods[0](x)))))
+        got = mlp3_forward(mods, x)
+    torch.testing.assert_close(got, ref, rtol=2e-5, atol=2e-5)
+    # the weight pack follows in-place updates (optimizer steps bump the version counters)
+    with torch.no_grad():
+        mods[2].weight.mul_(0.5)
+        ref = mods[4](torch.relu(mods[2](torch.relu(mods[0](x)))))
+        got = mlp3_forward(mods, x)
+    torch.testing.assert_close(got, ref, rtol=2e-5, atol=2e-5)
 
 
 def test_gaussian_sample_kernel_matches_torch_formula():
