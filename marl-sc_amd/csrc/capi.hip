@@ -759,14 +759,16 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
 
 int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
                           int32_t out_dim, const float* w1p, const float* b1, const float* w2p, const float* b2,
-                          const float* w3p, const float* b3, float* out, msc_stream_t stream) {
+                          const float* w3p, const float* b3, float* out, const float* pre1, int32_t pre1_group,
+                          msc_stream_t stream) {
+  if (pre1 && pre1_group < 1) return set_err(-1, "pre1_group %d must be >= 1", pre1_group);
   if (!x || !w1p || !b1 || !w2p || !b2 || !w3p || !b3 || !out) return set_err(-1, "null argument");
   if (n_rows < 0 || in_dim < 1 || in_dim > 1024 || out_dim < 1 || out_dim > 32)
     return set_err(-1, "bad shape (n_rows %lld, in_dim %d, out_dim %d)", (long long)n_rows, in_dim, out_dim);
   if (!(hidden1 == hidden2 && (hidden1 == 64 || hidden1 == 128 || hidden1 == 256)))
     return set_err(-1, "hidden sizes %d, %d: the fused MLP supports [64, 64], [128, 128] and [256, 256]", hidden1, hidden2);
-  HIP_TRY(launch_mlp3_relu(x, n_rows, in_dim, hidden1, hidden2, out_dim, w1p, b1, w2p, b2, w3p, b3, out,
-                           (hipStream_t)stream));
+  HIP_TRY(launch_mlp3_relu(x, n_rows, in_dim, hidden1, hidden2, out_dim, w1p, b1, w2p, b2, w3p, b3, out, pre1,
+                           pre1 ? pre1_group : 1, (hipStream_t)stream));
   return 0;
 }
 

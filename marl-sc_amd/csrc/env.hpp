@@ -131,7 +131,7 @@ hipError_t launch_gae(const float* r, const float* v, const float* nv, const uin
 hipError_t launch_adv_normalize(float* adv, int64_t n, int32_t n_groups, const double* stats, hipStream_t st);
 hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, int KO, const float* w1p, const float* b1,
                             const float* w2p, const float* b2, const float* w3p, const float* b3, float* out,
-                            hipStream_t st);
+                            const float* pre1, int grp, hipStream_t st);
 hipError_t launch_gauss_sample(const float* mean, const float* log_std, int32_t ls_rows, float floor_, const float* eps,
                                int64_t N, int32_t K, float* act, float* logp, float* clipped, hipStream_t st);
 

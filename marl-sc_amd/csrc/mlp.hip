@@ -29,36 +29,77 @@ typedef float mlp_f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ int mfma_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // NT1 / NT2: hidden tiles of 32 units; P: output tiles of layer 2 held at once (register budget:
-// 16 NT1 + 16 P + 16 accumulators + 4 P weight registers per lane)
+// 16 NT1 + 16 P + 16 accumulators + 2 x 4 P weight registers per lane).
+// Weight fragments are software-pipelined one step ahead (the loads of step s + 1 are issued before
+// the MFMAs of step s): with one wave per SIMD nothing else hides an L2 round trip, and a wait on
+// each step's own loads cost ~35 % of the MFMA time.
 template <int NT1, int NT2, int P, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mlp3_relu_kernel(
-    const float* __restrict__ x, int64_t n, int L, int KS1, const float* __restrict__ w1p, const float* __restrict__ b1,
+    const float* __restrict__ x, int64_t n, int L, int KS1, const float4* __restrict__ w1p, const float* __restrict__ b1,
     const float4* __restrict__ w2p, const float* __restrict__ b2, const float4* __restrict__ w3p,
-    const float* __restrict__ b3, int KO, float* __restrict__ out, int prio) {
+    const float* __restrict__ b3, int KO, float* __restrict__ out, const float* __restrict__ pre1, int grp, int prio) {
   static_assert(NT2 % P == 0, "layer-2 passes");
+  constexpr int S4 = NT1 * 4;  // layer-2 k steps of 4 MFMAs (2 hidden units each)
   // the policy forward is on the rollout's critical path (step t + 1 needs its actions), the
   // pipelined demand kernel of step t + 1 (priorities 1-2) is not: issue ahead of it
   if (prio) __builtin_amdgcn_s_setprio(3);
-  constexpr int S = NT1 * 16;  // layer-2 k steps (2 hidden units each)
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (tile * 32 >= n) return;  // wave-uniform (no block-level synchronisation below)
   const int64_t j = tile * 32 + (lane & 31);
   const bool jv = j < n;
+  const int M4 = (KS1 + 3) / 4;  // layer-1 k steps of 4 MFMAs
 
-  // layer 1: H1^T = W1 X^T + b1; lane half h feeds features [h KS1, h KS1 + KS1) of its sample
+  // layer 1: H1^T = W1 X^T + b1 (+ pre1 of the sample's group); lane half h feeds features
+  // h KS1 + m, m < KS1, of its sample
   mlp_f32x16 a1[NT1];
 #pragma unroll
   for (int t = 0; t < NT1; t++)
 #pragma unroll
     for (int r = 0; r < 16; r++) a1[t][r] = b1[t * 32 + mfma_row(r, h)];
-  const float* xr = x + (jv ? j : 0) * (int64_t)L;
-  for (int m = 0; m < KS1; m++) {
-    const int k = h * KS1 + m;
-    const float xv = (jv && k < L) ? xr[k] : 0.0f;
+  if (pre1 != nullptr) {  // a first-layer term shared by grp consecutive rows (MAPPO critic: the env's global block)
+    const float* pg = pre1 + ((jv ? j : 0) / grp) * (int64_t)(NT1 * 32);
 #pragma unroll
     for (int t = 0; t < NT1; t++)
-      a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w1p[((int64_t)t * KS1 + m) * 64 + lane], xv, a1[t], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 16; r++) a1[t][r] += pg[t * 32 + mfma_row(r, h)];
+  }
+  const float* xr = x + (jv ? j : 0) * (int64_t)L;
+  auto load_x = [&](int m4, float (&xv)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int m = m4 * 4 + i, k = h * KS1 + m;
+      xv[i] = (jv && m < KS1 && k < L) ? xr[k] : 0.0f;
+    }
+  };
+  {
+    float xc[4], xn[4];
+    float4 wc[NT1], wn[NT1];
+    load_x(0, xc);
+#pragma unroll
+    for (int t = 0; t < NT1; t++) wc[t] = w1p[((int64_t)t * M4) * 64 + lane];
+    for (int m4 = 0; m4 < M4; m4++) {
+      const bool more = m4 + 1 < M4;
+      if (more) {
+        load_x(m4 + 1, xn);
+#pragma unroll
+        for (int t = 0; t < NT1; t++) wn[t] = w1p[((int64_t)t * M4 + m4 + 1) * 64 + lane];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+#pragma unroll
+      for (int t = 0; t < NT1; t++) {
+        a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[t].x, xc[0], a1[t], 0, 0, 0);
+        a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[t].y, xc[1], a1[t], 0, 0, 0);
+        a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[t].z, xc[2], a1[t], 0, 0, 0);
+        a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[t].w, xc[3], a1[t], 0, 0, 0);
+      }
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) xc[i] = xn[i];
+#pragma unroll
+        for (int t = 0; t < NT1; t++) wc[t] = wn[t];
+      }
+    }
   }
 #pragma unroll
   for (int t = 0; t < NT1; t++)
@@ -73,6 +114,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     const int row = mfma_row(r, h);
     a3[r] = row < KO ? b3[row] : 0.0f;
   }
+  float4 w[2][P];  // [step parity][tile]: the fragments of step s4 and s4 + 1
+#pragma unroll
+  for (int q = 0; q < P; q++) w[0][q] = w2p[((int64_t)q * S4) * 64 + lane];
 #pragma unroll
   for (int p = 0; p < NT2 / P; p++) {
     mlp_f32x16 a2[P];
@@ -81,30 +125,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
       for (int r = 0; r < 16; r++) a2[q][r] = b2[(p * P + q) * 32 + mfma_row(r, h)];
 #pragma unroll
-    for (int s4 = 0; s4 < S / 4; s4++) {
-      float4 w[P];
+    for (int s4 = 0; s4 < S4; s4++) {
+      const int cb = (p * S4 + s4) & 1;
+      // prefetch: the next step of this pass, or the first step of the next pass
+      if (s4 + 1 < S4) {
 #pragma unroll
-      for (int q = 0; q < P; q++) w[q] = w2p[((int64_t)(p * P + q) * (S / 4) + s4) * 64 + lane];
+        for (int q = 0; q < P; q++) w[cb ^ 1][q] = w2p[((int64_t)(p * P + q) * S4 + s4 + 1) * 64 + lane];
+      } else if (p + 1 < NT2 / P) {
+#pragma unroll
+        for (int q = 0; q < P; q++) w[cb ^ 1][q] = w2p[((int64_t)((p + 1) * P + q) * S4) * 64 + lane];
+      }
+      // the scheduler would otherwise sink the prefetch into the registers this step frees last,
+      // i.e. 8 MFMAs before their use instead of 4 P
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int s = s4 * 4 + i;
         const float bv = a1[s / 16][s % 16];
 #pragma unroll
         for (int q = 0; q < P; q++) {
-          const float wv = i == 0 ? w[q].x : i == 1 ? w[q].y : i == 2 ? w[q].z : w[q].w;
+          const float4& wq = w[cb][q];
+          const float wv = i == 0 ? wq.x : i == 1 ? wq.y : i == 2 ? wq.z : wq.w;
           a2[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv, bv, a2[q], 0, 0, 0);
         }
       }
     }
+    // layer 3 on this pass's slice: the fragments of tile q + 1 are in flight during tile q
+    float4 w3[2][4];
+#pragma unroll
+    for (int r4 = 0; r4 < 4; r4++) w3[0][r4] = w3p[((int64_t)(p * P) * 4 + r4) * 64 + lane];
 #pragma unroll
     for (int q = 0; q < P; q++) {
+      if (q + 1 < P) {
+#pragma unroll
+        for (int r4 = 0; r4 < 4; r4++) w3[(q + 1) & 1][r4] = w3p[((int64_t)(p * P + q + 1) * 4 + r4) * 64 + lane];
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r4 = 0; r4 < 4; r4++) {
-        const float4 w = w3p[((int64_t)(p * P + q) * 4 + r4) * 64 + lane];
-        a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, fmaxf(a2[q][r4 * 4 + 0], 0.0f), a3, 0, 0, 0);
-        a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, fmaxf(a2[q][r4 * 4 + 1], 0.0f), a3, 0, 0, 0);
-        a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, fmaxf(a2[q][r4 * 4 + 2], 0.0f), a3, 0, 0, 0);
-        a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, fmaxf(a2[q][r4 * 4 + 3], 0.0f), a3, 0, 0, 0);
+        const float4 wq = w3[q & 1][r4];
+        a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(wq.x, fmaxf(a2[q][r4 * 4 + 0], 0.0f), a3, 0, 0, 0);
+        a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(wq.y, fmaxf(a2[q][r4 * 4 + 1], 0.0f), a3, 0, 0, 0);
+        a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(wq.z, fmaxf(a2[q][r4 * 4 + 2], 0.0f), a3, 0, 0, 0);
+        a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(wq.w, fmaxf(a2[q][r4 * 4 + 3], 0.0f), a3, 0, 0, 0);
       }
     }
   }
@@ -137,16 +200,17 @@ static int mlp_prio() {
 
 hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, int KO, const float* w1p, const float* b1,
                             const float* w2p, const float* b2, const float* w3p, const float* b3, float* out,
-                            hipStream_t st) {
+                            const float* pre1, int grp, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const int KS1 = (L + 1) / 2;
   const int64_t tiles = (n + 31) / 32;
   const dim3 grid((unsigned)((tiles + 3) / 4)), block(256);
+  const float4* w1 = reinterpret_cast<const float4*>(w1p);
   const float4* w2 = reinterpret_cast<const float4*>(w2p);
   const float4* w3 = reinterpret_cast<const float4*>(w3p);
 #define MSC_MLP_LAUNCH(NT1, NT2, P, WPE)                                                                          \
-  hipLaunchKernelGGL((mlp3_relu_kernel<NT1, NT2, P, WPE>), grid, block, 0, st, x, n, L, KS1, w1p, b1, w2, b2, w3, b3, \
-                     KO, out, mlp_prio())
+  hipLaunchKernelGGL((mlp3_relu_kernel<NT1, NT2, P, WPE>), grid, block, 0, st, x, n, L, KS1, w1, b1, w2, b2, w3, b3, \
+                     KO, out, pre1, grp, mlp_prio())
   if (H1 == 256 && H2 == 256) {
     if (mlp_p8() == 8) MSC_MLP_LAUNCH(8, 8, 8, 1);
     else MSC_MLP_LAUNCH(8, 8, 4, 2);

@@ -114,7 +114,7 @@ def lib() -> C.CDLL:
     L.msc_env_set_episode_counters.argtypes = [vp, vp]
     L.msc_gaussian_sample.argtypes = [vp, vp, C.c_int32, C.c_float, vp, C.c_int64, C.c_int32, vp, vp, vp, vp]
     L.msc_mlp3_relu_forward.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp, vp, vp,
-                                        vp, vp, vp]
+                                        vp, vp, vp, C.c_int32, vp]
     L.msc_seedseq_u32.argtypes = [P(C.c_uint32), C.c_int32]
     L.msc_seedseq_u32.restype = C.c_uint32
     L.msc_last_error.restype = C.c_char_p

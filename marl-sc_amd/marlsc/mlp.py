@@ -39,14 +39,15 @@ def _index_maps(L: int, H1: int, H2: int, KO: int, device) -> Tuple[torch.Tensor
     if key in _IDX:
         return _IDX[key]
     KS1 = (L + 1) // 2
+    M4 = (KS1 + 3) // 4
     lane = torch.arange(64, device=device)
     c, h = lane & 31, lane >> 5
-    # w1p[t][m][lane] = W1[32 t + c][h KS1 + m]  (0 past in_dim)
-    t = torch.arange(H1 // 32, device=device)[:, None, None]
-    m = torch.arange(KS1, device=device)[None, :, None]
-    f = h * KS1 + m
-    i1 = ((t * 32 + c) * L + f.clamp(max=L - 1)).reshape(-1)
-    v1 = (f < L).expand(H1 // 32, KS1, 64).reshape(-1)
+    # w1p[t][m4][lane][i] = W1[32 t + c][h KS1 + m], m = 4 m4 + i  (0 for m >= KS1 or past in_dim)
+    t = torch.arange(H1 // 32, device=device)[:, None, None, None]
+    m = torch.arange(M4, device=device)[None, :, None, None] * 4 + torch.arange(4, device=device)[None, None, None, :]
+    f = h[None, None, :, None] * KS1 + m
+    i1 = ((t * 32 + c[None, None, :, None]) * L + f.clamp(max=L - 1)).reshape(-1)
+    v1 = ((f < L) & (m < KS1)).expand(H1 // 32, M4, 64, 4).reshape(-1)
     # w2p[t2][s4][lane][i] = W2[32 t2 + c][32 t1 + rho(r, h)], s = 4 s4 + i = 16 t1 + r
     S = (H1 // 32) * 16
     t2 = torch.arange(H2 // 32, device=device)[:, None, None, None]
@@ -97,20 +98,25 @@ class _Pack:
         self.key, self.tensors = None, None
 
 
-def mlp3_forward(mods, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """The fused kernel over x [..., L] (f32 CUDA) -> [..., KO]; mods as accepted by fusable()."""
+def mlp3_forward(mods, x: torch.Tensor, out: Optional[torch.Tensor] = None, *, w1: Optional[torch.Tensor] = None,
+                 pre1: Optional[torch.Tensor] = None, group: int = 1) -> torch.Tensor:
+    """The fused kernel over x [..., L] (f32 CUDA) -> [..., KO]; mods as accepted by fusable().
+    w1: a first-layer weight to use instead of mods[0].weight (e.g. its local-feature columns);
+    pre1 [rows / group, H1]: added to the first layer's pre-activation of row n as pre1[n // group]."""
     l1, _, l2, _, l3 = mods
-    L, KO = l1.in_features, l3.out_features
+    w1 = l1.weight if w1 is None else w1
+    L, KO = w1.shape[1], l3.out_features
     if x.shape[-1] != L:
         raise ValueError(f"input has {x.shape[-1]} features, the MLP expects {L}")
-    # pack cache on the first Linear: rebuilt when any weight changes (version counters) or moves
-    pk = getattr(l1, "_msc_pack", None)
-    if pk is None:
-        pk = _Pack()
-        l1._msc_pack = pk
-    key = tuple((p.data_ptr(), p._version) for p in (l1.weight, l2.weight, l3.weight))
+    # pack cache on the first Linear (one per first-layer weight view): rebuilt when any weight
+    # changes (version counters) or moves
+    packs = getattr(l1, "_msc_packs", None)
+    if packs is None:
+        packs = l1._msc_packs = {}
+    pk = packs.setdefault((w1.shape, w1.stride(), w1.storage_offset()), _Pack())
+    key = tuple((p.data_ptr(), p._version) for p in (w1, l2.weight, l3.weight))
     if pk.key != key:
-        pk.tensors = pack_mlp3(l1.weight, l2.weight, l3.weight)
+        pk.tensors = pack_mlp3(w1, l2.weight, l3.weight)
         pk.key = key
     w1p, w2p, w3p = pk.tensors
     lead = x.shape[:-1]
@@ -118,11 +124,15 @@ def mlp3_forward(mods, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> t
     if xf.dtype != torch.float32 or not xf.is_contiguous():
         xf = xf.float().contiguous()
     n = xf.shape[0]
+    if pre1 is not None:
+        pre1 = pre1.float().contiguous()
+        if group < 1 or n % group or pre1.shape != (n // group, l1.out_features):
+            raise ValueError(f"pre1 must be [{n // max(group, 1)}, {l1.out_features}] for {n} rows in groups of {group}")
     if out is None:
         out = torch.empty((n, KO), device=x.device, dtype=torch.float32)
     b1, b2, b3 = (m.bias.detach().float().contiguous() for m in (l1, l2, l3))
-    vp = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    vp = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
     abi.check(abi.lib().msc_mlp3_relu_forward(vp(xf), n, L, l1.out_features, l2.out_features, KO, vp(w1p), vp(b1),
-                                              vp(w2p), vp(b2), vp(w3p), vp(b3), vp(out),
+                                              vp(w2p), vp(b2), vp(w3p), vp(b3), vp(out), vp(pre1), int(group),
                                               C.c_void_p(torch.cuda.current_stream().cuda_stream)))
     return out.reshape(*lead, KO)

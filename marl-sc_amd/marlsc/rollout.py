@@ -147,6 +147,13 @@ def split_global_mlp(mlp: nn.Sequential, local_obs: torch.Tensor, agent: Optiona
     first = mlp[0]
     W, L = local_obs.shape[-2], local_obs.shape[-1]
     glob = local_obs.reshape(*local_obs.shape[:-2], W * L)
+    mods = list(mlp)
+    if (agent is None and _FUSED and mlp3.ENABLED and local_obs.is_cuda and local_obs.dtype == torch.float32
+            and not torch.is_grad_enabled() and mlp3.fusable(mods)):
+        # the whole critic as one f32-MFMA kernel over the E*W rows, with the per-env global block
+        # (one GEMM over E rows) added to the first layer of each of the env's W rows
+        g = torch.nn.functional.linear(glob.reshape(-1, W * L), first.weight[:, L:])  # b1: in the kernel
+        return mlp3_forward(mods, local_obs, w1=first.weight[:, :L], pre1=g, group=W)
     g = torch.nn.functional.linear(glob, first.weight[:, L:])
     if agent is None:
         h = torch.nn.functional.linear(local_obs, first.weight[:, :L], first.bias) + g.unsqueeze(-2)
