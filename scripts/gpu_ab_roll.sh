@@ -3,10 +3,8 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests/test_gpu_rollout.py -q -x -p no:cacheprovider > gpurun_out/pytest_roll.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -n 3 gpurun_out/pytest_roll.log; [ $rc -eq 0 ] || exit $rc
-for cfg in "1 1" "2 1" "2 0" "4 1" "4 0" "1 1" "2 1"; do
-  set -- $cfg
+for cfg in ${AB_CFGS:-1:1 2:1 2:0 4:1 1:1 2:1}; do
+  set -- ${cfg%:*} ${cfg#*:}
   MSC_ROLLOUT_PIPELINE=$2 timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --rollout-lanes $1 > gpurun_out/ab_roll_$1_$2.log 2>&1 || exit $?
   echo "lanes=$1 pipe=$2 $(tail -n 1 gpurun_out/ab_roll_$1_$2.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["rollout"]["value"], d["rollout"]["ms_per_step"])')"
 done
