@@ -267,6 +267,19 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     }
     c.alloc_lpe = 0;
     if (const char* lp = getenv("MSC_ALLOC_LPE")) c.alloc_lpe = atoi(lp);
+    // group kernel over empirical demand: a wave runs as many order iterations as its busiest env,
+    // and trace order counts spread widely (C5: 200-1,000 per step), so the envs are visited in
+    // descending order of this step's count (one counting-sort launch; results do not depend on
+    // the order, every env is independent). MSC_ALLOC_SORT=0|1 forces it off / on.
+    c.alloc_sort = (c.alloc_impl == 1 && d->demand_type == MSC_DEMAND_EMPIRICAL) ? 1 : 0;
+    if (const char* so = getenv("MSC_ALLOC_SORT")) c.alloc_sort = c.alloc_impl == 1 && atoi(so) != 0 ? 1 : 0;
+    int64_t maxc = order_cap;
+    if (d->demand_type == MSC_DEMAND_EMPIRICAL) {
+      maxc = 0;
+      for (int i = 0; i < c.tr_rows; i++) maxc = std::max<int64_t>(maxc, toff[i + 1] - toff[i]);
+    }
+    c.sort_shift = 0;
+    while ((maxc >> c.sort_shift) >= SORT_BUCKETS) c.sort_shift++;
   }
 
   TablePack tp;
@@ -363,6 +376,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   const size_t a_orig = slot(sizeof(uint32_t) * E);
   const size_t a_root = slot(sizeof(uint32_t) * E);
   const size_t a_emp = slot(sizeof(int32_t) * E);
+  const size_t a_perm = slot(sizeof(int32_t) * E);
   const size_t a_err = slot(sizeof(uint32_t) * 4);
   const size_t a_sht = slot(sizeof(int32_t) * WK * E);
   const size_t a_shh = slot(sizeof(int32_t) * WK * E);
@@ -389,6 +403,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   s.orig_root = (uint32_t*)(ab + a_orig);
   s.root = (uint32_t*)(ab + a_root);
   s.emp_start = (int32_t*)(ab + a_emp);
+  s.perm = (int32_t*)(ab + a_perm);
   s.err = (uint32_t*)(ab + a_err);
   s.sc_sht = (int32_t*)(ab + a_sht);
   s.sc_shh = (int32_t*)(ab + a_shh);

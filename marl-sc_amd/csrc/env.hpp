@@ -38,6 +38,8 @@ struct EnvConst {
   int32_t demand_uni;   // 1: Poisson parameters equal across regions (demand_unit_kernel<UNI>)
   int32_t alloc_impl;   // phase B: 0 = one env per lane (alloc_lane_kernel); 1 = one env per lane group (step_b_kernel)
   int32_t alloc_lpe;    // alloc_lane_kernel lanes per env forced by MSC_ALLOC_LPE (1, 2, 4); 0 = by env count
+  int32_t alloc_sort;   // step_b_kernel visits envs in descending order of this step's order count (perm)
+  int32_t sort_shift;   // order count >> sort_shift = bucket (< SORT_BUCKETS)
   uint32_t flags;
   int64_t E;
   double scale, alpha, hold_scalar, pen_scalar;
@@ -82,6 +84,7 @@ struct EnvState {
   MSC_G uint32_t* orig_root; // [E] SeedManager._original_root_seed
   MSC_G uint32_t* root;      // [E] SeedManager.root_seed
   MSC_G int32_t* emp_start;  // [E] EmpiricalDemandSampler window start row (-1: not drawn)
+  MSC_G int32_t* perm;       // [E] allocation visiting order (alloc_sort): envs by descending order count
   uint4* orders;       // [order_cap][E][NV] per-step order records (Poisson sampler output)
   MSC_G int32_t* n_orders;   // [E]
   // step phase scratch (step_a/b/c kernels): shipped total / home [WK][E], penalty / outbound /
@@ -119,6 +122,7 @@ hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask,
                         int32_t flags, float* obs, hipStream_t st);
 hipError_t launch_step(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen_demand, hipStream_t st);
 hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st);
+constexpr int SORT_BUCKETS = 1024;
 // alloc_kernels.hip
 hipError_t launch_alloc_lane(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
 hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hipStream_t st);

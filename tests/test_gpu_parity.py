@@ -16,19 +16,30 @@ pytestmark = pytest.mark.gpu
 REW_ATOL = 1e-6
 
 
-@pytest.fixture(params=["lane", "group"])
+def _set_alloc(monkeypatch, param):
+    impl, _, opt = param.partition("_")
+    monkeypatch.setenv("MSC_ALLOC_IMPL", impl[:4] if impl != "group" else "group")
+    monkeypatch.setenv("MSC_ALLOC_LPE", impl[4:] if impl.startswith("lane") and impl[4:] else "0")
+    # group kernel: envs visited in descending order of their order count (default for empirical
+    # demand), forced on ("sorted") or off ("unsorted")
+    if opt:
+        monkeypatch.setenv("MSC_ALLOC_SORT", "1" if opt == "sorted" else "0")
+    else:
+        monkeypatch.delenv("MSC_ALLOC_SORT", raising=False)
+
+
+@pytest.fixture(params=["lane", "group", "group_sorted"])
 def alloc_impl(request, monkeypatch):
     # both phase-B allocation kernels (one env per lane / one env per lane group) against the same
     # references; msc_env_create picks by shape otherwise (small test batches would get the group one)
-    monkeypatch.setenv("MSC_ALLOC_IMPL", request.param)
+    _set_alloc(monkeypatch, request.param)
     return request.param
 
 
-@pytest.fixture(params=["lane", "lane2", "lane4", "group"])
+@pytest.fixture(params=["lane", "lane2", "lane4", "group", "group_sorted", "group_unsorted"])
 def alloc_impl_lpe(request, monkeypatch):
     # as alloc_impl, plus the lane kernel's 2 / 4 lanes-per-env forms (A/B; >= 8 warehouses)
-    monkeypatch.setenv("MSC_ALLOC_IMPL", request.param[:4] if request.param != "group" else "group")
-    monkeypatch.setenv("MSC_ALLOC_LPE", request.param[4:] or "0")
+    _set_alloc(monkeypatch, request.param)
     return request.param
 
 
