@@ -1094,6 +1094,9 @@ __device__ __forceinline__ double group_np_sum(double v, int n) {
 #ifndef MSC_SB_WPE
 #define MSC_SB_WPE 5
 #endif
+#ifndef MSC_SB_BPERM
+#define MSC_SB_BPERM 0  // 1: winner's fill broadcast by ds_bpermute (A/B, lost at C5: 0.908 vs 0.903 ms/step)
+#endif
 
 // This step's order count of env e (what step_b_kernel iterates over).
 __device__ __forceinline__ int step_order_count(const EnvConst& c, const EnvState& s, int64_t e) {
@@ -1419,8 +1422,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
 #pragma unroll
       for (int j = 0; j < NP; j++)
         pk[j] = (unsigned)fl[2 * j] | (2 * j + 1 < K ? (unsigned)fl[2 * j + 1] << 16 : 0u);
+#if MSC_SB_BPERM
+      // one ds_bpermute per word from the winner lane (3 LDS-crossbar reads instead of an OR
+      // butterfly of log2(GW) DPP steps per word)
+      {
+        const int src = (gbase + bw) << 2;
+#pragma unroll
+        for (int j = 0; j < NP; j++) pk[j] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)pk[j]);
+      }
+#else
 #pragma unroll
       for (int j = 0; j < NP; j++) pk[j] = (unsigned)group_reduce<GW>((int)pk[j], [](int a, int b) { return a | b; });
+#endif
       bool done = true;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) {
