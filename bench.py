@@ -67,6 +67,13 @@ def algorithmic_bytes(spec, mean_orders: float):
     return demand, step
 
 
+def _mlp_traffic(tj: Path, key: str):
+    """HBM bytes per launch of the fused MLP from its rocprofv3 PMC passes (tools/bench_mlp.py), if recorded."""
+    if not tj.exists():
+        return None
+    return json.loads(tj.read_text()).get("mlp3_relu_kernel", {}).get(key, {}).get("traffic")
+
+
 def cpu_baseline(spec, seconds: float):
     """The C oracle on the host's cores (<= 16 threads), plus a 1-core figure."""
     out = _cpu_rate(spec, seconds, max(1, min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
@@ -276,6 +283,7 @@ def main():
             mlp_line = {"kernel": "mlp3_relu_kernel", "bound": "mfma", "achieved": round(fl / t_mlp / 1e12, 2),
                         "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(fl / t_mlp / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
                         "flops_per_launch": int(fl), "ms": round(t_mlp * 1e3, 4),
+                        "traffic": _mlp_traffic(Path(args.traffic_json), f"{spec.local_obs_dim}x{H1}x{H2}x{spec.K}x{N}"),
                         "shape": f"actor {spec.local_obs_dim}-{H1}-{H2}-{spec.K} over N={N} rows (E x W of one rollout step), "
                                  f"f32 MFMA, timed alone"}
             del xg, yo
