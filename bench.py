@@ -134,8 +134,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one process per GPU over RCCL ("nccl" on ROCm); MSC_DIST_BACKEND=gloo rehearses the
+        # multi-rank path with every rank on the visible GPU(s) (ranks share a card when fewer)
+        backend = os.environ.get("MSC_DIST_BACKEND", "nccl")
+        dev_i = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_i)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_i))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     if rank == 0:
