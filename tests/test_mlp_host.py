@@ -1,0 +1,83 @@
+"""Host test of the fused policy MLP's weight packing (marlsc/mlp.py:pack_mlp3): a numpy emulation of
+the kernel's v_mfma_f32_32x32x2_f32 data flow (csrc/mlp.hip) over the packed fragments reproduces
+the torch MLP (float64), so the lane / register maps of the packing are checked without a GPU.
+MFMA operand maps (cdna_hip_programming.md, f32 32x32x2): lane l holds A[l & 31][k = l >> 5] and
+B[k = l >> 5][l & 31]; accumulator register r of lane l is D[(r & 3) + 8 (r >> 2) + 4 (l >> 5)][l & 31]."""
+import numpy as np
+import pytest
+import torch
+
+from marlsc.mlp import fusable, pack_mlp3
+from marlsc.rollout import MLP
+
+
+def _mfma(a_lane, b_lane, d):
+    A = np.zeros((32, 2))
+    B = np.zeros((2, 32))
+    for lane in range(64):
+        A[lane & 31, lane >> 5] = a_lane[lane]
+        B[lane >> 5, lane & 31] = b_lane[lane]
+    return d + A @ B
+
+
+def _rho(r, h):
+    return (r & 3) + 8 * (r >> 2) + 4 * h
+
+
+def _regs(tile, r):
+    """Register r of every lane of a [32 rows x 32 samples] accumulator tile."""
+    return np.array([tile[_rho(r, lane >> 5), lane & 31] for lane in range(64)])
+
+
+def _emulate(mlp, x):
+    l1, _, l2, _, l3 = list(mlp)
+    H1, L = l1.weight.shape
+    H2, KO = l2.weight.shape[0], l3.weight.shape[0]
+    KS1 = (L + 1) // 2
+    M4 = (KS1 + 3) // 4
+    w1p, w2p, w3p = (t.double().numpy() for t in pack_mlp3(l1.weight, l2.weight, l3.weight))
+    w1p = w1p.reshape(H1 // 32, M4, 64, 4)
+    w2p = w2p.reshape(H2 // 32, H1 // 8, 64, 4)
+    w3p = w3p.reshape(H2 // 8, 64, 4)
+    b1, b2, b3 = (m.bias.detach().double().numpy() for m in (l1, l2, l3))
+    n = x.shape[0]
+    assert n == 32  # one wave
+    h1 = []
+    for t in range(H1 // 32):
+        d = np.zeros((32, 32))
+        for m in range(M4 * 4):
+            xb = [x[lane & 31, (lane >> 5) * KS1 + m] if m < KS1 and (lane >> 5) * KS1 + m < L else 0.0
+                  for lane in range(64)]
+            d = _mfma(w1p[t, m // 4, :, m % 4], xb, d)
+        h1.append(np.maximum(d + b1[t * 32:(t + 1) * 32, None], 0))
+    h2 = []
+    for t2 in range(H2 // 32):
+        d = np.zeros((32, 32))
+        for s in range((H1 // 32) * 16):
+            d = _mfma(w2p[t2, s // 4, :, s % 4], _regs(h1[s // 16], s % 16), d)
+        h2.append(np.maximum(d + b2[t2 * 32:(t2 + 1) * 32, None], 0))
+    d = np.zeros((32, 32))
+    for q in range((H2 // 32) * 4):
+        for i in range(4):
+            d = _mfma(w3p[q, :, i], _regs(h2[q // 4], (q % 4) * 4 + i), d)
+    return (d[:KO] + b3[:, None]).T
+
+
+@pytest.mark.parametrize("L,H,KO", [(34, 64, 5), (7, 64, 1), (42, 128, 3)])
+def test_packed_fragments_reproduce_the_mlp(L, H, KO):
+    torch.manual_seed(L * H + KO)
+    mlp = MLP(L, KO, {"hidden_sizes": [H, H]})
+    assert fusable(list(mlp))
+    x = torch.randn(32, L, dtype=torch.float64)
+    got = _emulate(mlp, x.numpy())
+    ref = mlp.double()(x).detach().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_fusable_shapes():
+    assert fusable(list(MLP(34, 5, {"hidden_sizes": [256, 256]})))
+    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [256, 128]})))    # unequal hidden sizes
+    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [96, 96]})))      # not 64 / 128 / 256
+    assert not fusable(list(MLP(34, 40, {"hidden_sizes": [64, 64]})))     # > 32 outputs
+    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [64, 64], "activation": "tanh"})))
+    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [64]})))
