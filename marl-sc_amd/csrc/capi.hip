@@ -777,6 +777,9 @@ int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_
                           const float* w3p, const float* b3, float* out, const float* pre1, int32_t pre1_group,
                           msc_stream_t stream) {
   if (pre1 && pre1_group < 1) return set_err(-1, "pre1_group %d must be >= 1", pre1_group);
+  // the kernel reads b1 / b2 / pre1 rows as float4
+  if (((uintptr_t)b1 | (uintptr_t)b2 | (uintptr_t)pre1 | (uintptr_t)w1p | (uintptr_t)w2p | (uintptr_t)w3p) & 15)
+    return set_err(-1, "b1, b2, pre1 and the packed weights must be 16-byte aligned");
   if (!x || !w1p || !b1 || !w2p || !b2 || !w3p || !b3 || !out) return set_err(-1, "null argument");
   if (n_rows < 0 || in_dim < 1 || in_dim > 1024 || out_dim < 1 || out_dim > 32)
     return set_err(-1, "bad shape (n_rows %lld, in_dim %d, out_dim %d)", (long long)n_rows, in_dim, out_dim);

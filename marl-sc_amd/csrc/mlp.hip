@@ -52,17 +52,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 
   // layer 1: H1^T = W1 X^T + b1 (+ pre1 of the sample's group); lane half h feeds features
   // h KS1 + m, m < KS1, of its sample
+  // (registers 4g .. 4g + 3 of a tile hold rows 8g + 4h .. 8g + 4h + 3: one float4 per group)
   mlp_f32x16 a1[NT1];
 #pragma unroll
   for (int t = 0; t < NT1; t++)
 #pragma unroll
-    for (int r = 0; r < 16; r++) a1[t][r] = b1[t * 32 + mfma_row(r, h)];
+    for (int g = 0; g < 4; g++) {
+      const float4 v = *reinterpret_cast<const float4*>(b1 + t * 32 + 8 * g + 4 * h);
+      a1[t][4 * g] = v.x, a1[t][4 * g + 1] = v.y, a1[t][4 * g + 2] = v.z, a1[t][4 * g + 3] = v.w;
+    }
   if (pre1 != nullptr) {  // a first-layer term shared by grp consecutive rows (MAPPO critic: the env's global block)
     const float* pg = pre1 + ((jv ? j : 0) / grp) * (int64_t)(NT1 * 32);
 #pragma unroll
     for (int t = 0; t < NT1; t++)
 #pragma unroll
-      for (int r = 0; r < 16; r++) a1[t][r] += pg[t * 32 + mfma_row(r, h)];
+      for (int g = 0; g < 4; g++) {
+        const float4 v = *reinterpret_cast<const float4*>(pg + t * 32 + 8 * g + 4 * h);
+        a1[t][4 * g] += v.x, a1[t][4 * g + 1] += v.y, a1[t][4 * g + 2] += v.z, a1[t][4 * g + 3] += v.w;
+      }
   }
   const float* xr = x + (jv ? j : 0) * (int64_t)L;
   auto load_x = [&](int m4, float (&xv)[4]) {
@@ -123,7 +130,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
     for (int q = 0; q < P; q++)
 #pragma unroll
-      for (int r = 0; r < 16; r++) a2[q][r] = b2[(p * P + q) * 32 + mfma_row(r, h)];
+      for (int g = 0; g < 4; g++) {
+        const float4 v = *reinterpret_cast<const float4*>(b2 + (p * P + q) * 32 + 8 * g + 4 * h);
+        a2[q][4 * g] = v.x, a2[q][4 * g + 1] = v.y, a2[q][4 * g + 2] = v.z, a2[q][4 * g + 3] = v.w;
+      }
 #pragma unroll
     for (int s4 = 0; s4 < S4; s4++) {
       const int cb = (p * S4 + s4) & 1;
@@ -185,7 +195,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 static int mlp_p8() {
   static const int v = [] {
     const char* e = getenv("MSC_MLP_P8");
-    return (e && atoi(e) == 4) ? 4 : 8;
+    return (e && (atoi(e) == 4 || atoi(e) == 2)) ? atoi(e) : 8;
   }();
   return v;
 }
@@ -213,7 +223,8 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
                      KO, out, pre1, grp, mlp_prio())
   if (H1 == 256 && H2 == 256) {
     if (mlp_p8() == 8) MSC_MLP_LAUNCH(8, 8, 8, 1);
-    else MSC_MLP_LAUNCH(8, 8, 4, 2);
+    else if (mlp_p8() == 4) MSC_MLP_LAUNCH(8, 8, 4, 2);
+    else MSC_MLP_LAUNCH(8, 8, 2, 2);
   } else if (H1 == 128 && H2 == 128) {
     MSC_MLP_LAUNCH(4, 4, 4, 2);
   } else if (H1 == 64 && H2 == 64) {
