@@ -81,3 +81,24 @@ def test_fusable_shapes():
     assert not fusable(list(MLP(34, 40, {"hidden_sizes": [64, 64]})))     # > 32 outputs
     assert not fusable(list(MLP(34, 5, {"hidden_sizes": [64, 64], "activation": "tanh"})))
     assert not fusable(list(MLP(34, 5, {"hidden_sizes": [64]})))
+
+
+def test_mlp3_abi_rejects_bad_arguments_before_any_launch():
+    # msc_mlp3_relu_forward validates its arguments on the host (no HIP call is made on these paths)
+    import ctypes as C
+    from marlsc import abi
+    L = abi.lib()
+    f = L.msc_mlp3_relu_forward
+    p = C.c_void_p(16)  # never dereferenced: every call below fails validation first
+    assert f(None, 8, 34, 256, 256, 5, p, p, p, p, p, p, p, None, 1, None) == -1
+    assert b"null" in L.msc_last_error()
+    assert f(p, 8, 34, 256, 128, 5, p, p, p, p, p, p, p, None, 1, None) == -1
+    assert b"hidden sizes" in L.msc_last_error()
+    assert f(p, 8, 34, 96, 96, 5, p, p, p, p, p, p, p, None, 1, None) == -1
+    assert f(p, 8, 34, 64, 64, 33, p, p, p, p, p, p, p, None, 1, None) == -1
+    assert b"out_dim" in L.msc_last_error()
+    assert f(p, 8, 34, 64, 64, 5, p, p, p, p, p, p, p, p, 0, None) == -1
+    assert b"pre1_group" in L.msc_last_error()
+    q = C.c_void_p(20)  # misaligned bias
+    assert f(p, 8, 34, 64, 64, 5, p, q, p, p, p, p, p, None, 1, None) == -1
+    assert b"aligned" in L.msc_last_error()
