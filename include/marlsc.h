@@ -196,6 +196,14 @@ int msc_env_generate_demand(msc_env* env, msc_stream_t stream);
  * way; 0 disables it (every step then runs demand + step back to back on the caller's stream). */
 int msc_env_set_pipelining(msc_env* env, int32_t enabled);
 
+/* Wave priority of the step chain (no reference counterpart: a scheduling hint). With enabled != 0
+ * the phase-A and phase-C kernels of msc_env_step run at s_setprio 3, like the allocation kernel,
+ * ahead of the pipelined demand kernel of the next step. For callers that run their own work between
+ * steps (a rollout's policy forward): the env step is then their critical path and the next step's
+ * demand has slack. Default 0 (env-only stepping: the demand kernel is the critical path).
+ * Synchronises the device. Results are identical either way. */
+int msc_env_set_chain_priority(msc_env* env, int32_t enabled);
+
 /* Per-launch device durations of the production path (for roofline accounting): with max_steps > 0
  * the next max_steps calls of msc_env_step bracket their demand launch and their step launch (the
  * step kernels of that call) with HIP events on the stream each runs on -- the caller's stream, or

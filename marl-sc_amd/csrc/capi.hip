@@ -595,6 +595,17 @@ int msc_env_set_pipelining(msc_env* env, int32_t enabled) {
   return 0;
 }
 
+int msc_env_set_chain_priority(msc_env* env, int32_t enabled) {
+  if (!env) return set_err(-1, "null env");
+  const int32_t v = enabled != 0 ? 1 : 0;
+  env->c.chain_prio = v;
+  HIP_TRY(hipSetDevice(env->device));
+  HIP_TRY(hipDeviceSynchronize());  // no launch in flight reads the descriptors being patched
+  for (int b = 0; b < 2; b++)
+    HIP_TRY(hipMemcpy(&env->dev[b].c.chain_prio, &v, sizeof v, hipMemcpyHostToDevice));
+  return 0;
+}
+
 int msc_env_set_timing(msc_env* env, int32_t max_steps) {
   if (!env) return set_err(-1, "null env");
   if (max_steps < 0) return set_err(-1, "max_steps < 0");

@@ -38,6 +38,7 @@ struct EnvConst {
   int32_t demand_uni;   // 1: Poisson parameters equal across regions (demand_unit_kernel<UNI>)
   int32_t alloc_impl;   // phase B: 0 = one env per lane (alloc_lane_kernel); 1 = one env per lane group (step_b_kernel)
   int32_t alloc_lpe;    // alloc_lane_kernel lanes per env forced by MSC_ALLOC_LPE (1, 2, 4); 0 = by env count
+  int32_t chain_prio;   // step_a / step_c waves at s_setprio 3 (msc_env_set_chain_priority)
   int32_t alloc_sort;   // step_b_kernel visits envs in descending order of this step's order count (perm)
   int32_t sort_shift;   // order count >> sort_shift = bucket (< SORT_BUCKETS)
   uint32_t flags;

@@ -936,6 +936,7 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __
   const int64_t E = c.E;
   const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;
   const int64_t e = (int64_t)blockIdx.x * BS + lane;
+  if (c.chain_prio) __builtin_amdgcn_s_setprio(3);  // the step chain is the caller's critical path
   const bool ev = e < E;
   const msc_step_info info = io.info;
   constexpr bool dbg = DBG;
@@ -1503,6 +1504,7 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __
   const int64_t E = c.E;
   const int wave = threadIdx.x / BS, lane = threadIdx.x % BS;
   if (MSC_SC_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SC_PRIO);
+  if (c.chain_prio) __builtin_amdgcn_s_setprio(3);  // the step chain is the caller's critical path
   const int64_t e = (int64_t)blockIdx.x * BS + lane;
   const bool act = wave < W && e < E;
   const int w = wave;

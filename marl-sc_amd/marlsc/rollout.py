@@ -221,13 +221,16 @@ def normalize_advantages(adv: torch.Tensor, stats: torch.Tensor) -> torch.Tensor
     return adv
 
 
+NOISE_CHUNK = 16  # rollout steps whose Gaussian noise is drawn in one launch
+
+
 class _Lane:
     """One env handle of a collector: its slice [e0, e1) of the buffers' env axis and the HIP stream
     its step chain (policy forward -> sampling -> env step) is issued on (None: the caller's)."""
 
     def __init__(self, env: VecInventoryEnv, e0: int, stream: Optional[torch.cuda.Stream], flat: Optional[torch.Tensor]):
         self.env, self.e0, self.e1, self.stream, self.flat = env, e0, e0 + env.n_envs, stream, flat
-        self.obs: Optional[torch.Tensor] = None
+        self.noise: Optional[torch.Tensor] = None
 
     def ctx(self):
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
@@ -255,7 +258,10 @@ class RolloutCollector:
         W, K, L = e0.W, e0.K, e0.local_obs_dim
         dev = e0.device
         self.E, self.N = E, E * W
-        self.obs = torch.empty((T, E, W, L), device=dev)
+        # T + 1 observation rows: the env writes step t's result straight into row t + 1 (no copy
+        # per step); `obs` is the first T rows, the last one is copied back into the env at the end
+        self._obs_all = torch.empty((T + 1, E, W, L), device=dev)
+        self.obs = self._obs_all[:T]
         self.actions = torch.empty((T, E, W, K), device=dev)
         self.logp = torch.empty((T, E, W), device=dev)
         self.rewards = torch.empty((T, E, W), device=dev)
@@ -282,36 +288,46 @@ class RolloutCollector:
         return ln.env.obs_flat(obs=obs, out=ln.flat) if self._need_flat else None
 
     def _step(self, ln: _Lane, t: int) -> None:
-        env, m, sl, obs = ln.env, self.module, slice(ln.e0, ln.e1), ln.obs
-        self.obs[t, sl].copy_(obs)
+        env, m, sl = ln.env, self.module, slice(ln.e0, ln.e1)
+        obs = self._obs_all[t, sl]
         full = self._full(ln, obs)
         mean, log_std = m.dist_inputs(obs, full)
         self.values[t, sl] = m.values(obs, full)
-        eps = torch.randn(mean.shape, device=mean.device, generator=self._gen)
+        # standard-normal noise for NOISE_CHUNK steps of the lane at once (one launch instead of one
+        # per step)
+        if t % NOISE_CHUNK == 0:
+            n = min(NOISE_CHUNK, self.T - t)
+            ln.noise = torch.randn((n,) + tuple(mean.shape), device=mean.device, generator=self._gen)
+        eps = ln.noise[t % NOISE_CHUNK]
         # sample, log-density and the env's clip in one HIP kernel (msc_gaussian_sample)
         # log_std [E, W, K] is a broadcast of one row (shared policy) or of W rows (per agent)
         a = gaussian_sample(mean.contiguous(), log_std[0], m.rc.logstd_floor, eps, self.actions[t, sl], self.logp[t, sl])
         may_end = env.may_truncate()
-        ln.obs, rew, trunc, final_obs = env.step(a)
-        self.rewards[t, sl] = rew
+        _, _, trunc, final_obs = env.step(a, obs_out=self._obs_all[t + 1, sl], rewards_out=self.rewards[t, sl])
         self.truncated[t, sl] = trunc.unsqueeze(-1)
         # truncation bootstrap: V(final_obs) for the envs whose episode ended at this step
-        # (skipped while the envs are known to be mid-episode in lockstep)
+        # (skipped while the envs are known to be mid-episode in lockstep; next_values is zeroed
+        # once per rollout)
         if may_end:
             full_f = self._full(ln, final_obs)
             self.next_values[t, sl] = torch.where(trunc.bool().unsqueeze(-1), m.values(final_obs, full_f),
                                                   torch.zeros((), device=final_obs.device))
-        else:
-            self.next_values[t, sl].zero_()
 
     @torch.no_grad()
     def collect(self, normalize: bool = True) -> Dict[str, torch.Tensor]:
         m, T = self.module, self.T
         main = torch.cuda.current_stream()
+        self.next_values.zero_()
         for ln in self._lanes:
-            ln.obs = ln.env.obs
+            if os.environ.get("MSC_ROLLOUT_CHAIN_PRIO", "0") != "0" and not getattr(ln, "prio_set", False):
+                # A/B: step chain ahead of the next step's demand kernel (neutral: 1.234 vs 1.228 ms
+                # per step; the step kernels wait for CU space, not for issue slots)
+                ln.env.set_chain_priority(True)
+                ln.prio_set = True
             if ln.stream is not None:
                 ln.stream.wait_stream(main)
+            with ln.ctx():
+                self._obs_all[0, ln.e0:ln.e1].copy_(ln.env.obs)
         # lanes interleaved per step on the host; each lane's chain is ordered on its own stream
         for t in range(T):
             for ln in self._lanes:
@@ -319,7 +335,9 @@ class RolloutCollector:
                     self._step(ln, t)
         for ln in self._lanes:
             with ln.ctx():
-                self.values[T, ln.e0:ln.e1] = m.values(ln.obs, self._full(ln, ln.obs))
+                last = self._obs_all[T, ln.e0:ln.e1]
+                self.values[T, ln.e0:ln.e1] = m.values(last, self._full(ln, last))
+                ln.env.obs.copy_(last)  # the env's own buffer holds the current observation again
             if ln.stream is not None:
                 main.wait_stream(ln.stream)
         N = self.N

@@ -97,10 +97,17 @@ class VecInventoryEnv:
         return self.obs
 
     def step(self, actions: torch.Tensor, *, want_final_obs: bool = True, want_f64: bool = False,
-             info: Optional[Dict[str, torch.Tensor]] = None):
+             info: Optional[Dict[str, torch.Tensor]] = None, obs_out: Optional[torch.Tensor] = None,
+             rewards_out: Optional[torch.Tensor] = None):
         """actions [E, W, K] float32 on the device. Returns (obs [E,W,L], rewards [E,W],
         truncated [E] bool-as-u8, final_obs [E,W,L] or None). Returned tensors are internal
-        buffers, overwritten by the next call."""
+        buffers, overwritten by the next call. obs_out / rewards_out (contiguous f32 [E,W,L] / [E,W]
+        on the device, e.g. a rollout buffer's row): written instead of the internal buffers, which
+        then keep their previous contents (`obs` is stale until the caller copies the latest back)."""
+        for name, t, shape in (("obs_out", obs_out, (self.n_envs, self.W, self.L)), ("rewards_out", rewards_out, (self.n_envs, self.W))):
+            if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device
+                                  or tuple(t.shape) != shape):
+                raise ValueError(f"{name} must be a contiguous float32 {shape} tensor on {self.device}")
         if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
             actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
         if actions.shape != (self.n_envs, self.W, self.K):
@@ -111,12 +118,14 @@ class VecInventoryEnv:
             for k, v in info.items():
                 setattr(s, k, C.cast(C.c_void_p(v.data_ptr()), C.POINTER(C.c_double if v.dtype == torch.float64 else C.c_int32)))
             si = C.byref(s)
+        obs = self.obs if obs_out is None else obs_out
+        rew = self.rewards if rewards_out is None else rewards_out
         abi.check(abi.lib().msc_env_step(
-            self._h, _p(actions), _p(self.obs), _p(self.rewards), _p(self.rewards_f64) if want_f64 else None,
+            self._h, _p(actions), _p(obs), _p(rew), _p(self.rewards_f64) if want_f64 else None,
             _p(self.truncated), _p(self.final_obs) if want_final_obs else None, si, _stream()))
         ts = getattr(self, "_t_sync", -1)
         self._t_sync = -1 if ts < 0 else (0 if ts + 1 >= self.spec.episode_length else ts + 1)
-        return self.obs, self.rewards, self.truncated, (self.final_obs if want_final_obs else None)
+        return obs, rew, self.truncated, (self.final_obs if want_final_obs else None)
 
     def may_truncate(self) -> bool:
         """Whether the next step() can end an episode (host-side lockstep tracking, no sync): False
@@ -131,6 +140,12 @@ class VecInventoryEnv:
     def set_pipelining(self, enabled: bool) -> None:
         """Toggle the library's automatic next-step demand pipelining (results are identical)."""
         abi.check(abi.lib().msc_env_set_pipelining(self._h, int(bool(enabled))))
+
+    def set_chain_priority(self, enabled: bool) -> None:
+        """Run the step chain's kernels ahead of the pipelined demand kernel (msc_env_set_chain_priority):
+        for callers whose own work between steps (a policy forward) makes the env step their critical
+        path. Results are identical either way."""
+        abi.check(abi.lib().msc_env_set_chain_priority(self._h, int(bool(enabled))))
 
     def set_timing(self, max_steps: int) -> None:
         """Bracket the demand / step launches of the next max_steps steps with HIP events on the
