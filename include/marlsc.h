@@ -286,12 +286,15 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
  * in_dim floats, in one kernel on the f32 MFMA (hidden activations stay in registers).
  * hidden1 == hidden2 in {64, 128, 256}; out_dim <= 32. Weights are passed in the packed fragment
  * order the kernel streams (marlsc/mlp.py:pack_mlp3 builds them from the torch [out, in] matrices):
- *   w1p [hidden1/32][ceil(ceil(in_dim/2)/4)][64][4], w2p [hidden2/32][hidden1/8][64][4], w3p [hidden2/8][64][4];
+ *   w1p [hidden1/32][ceil(ceil(in_dim/2)/4)][64][4], w2p [hidden2/32][hidden1/8][64][4], and w3p either
+ *   [hidden2/8][64][4] (MFMA output layer) or [hidden2/2][2][8] (VALU output layer, out_dim <= 8):
+ *   msc_mlp3_w3_layout(out_dim) says which (0 / 1; -1 for an unsupported out_dim);
  * biases b1 [hidden1], b2 [hidden2], b3 [out_dim] as in torch. x [n_rows][in_dim], out [n_rows][out_dim]:
  * f32 device buffers; stream-ordered. pre1 (optional, [n_rows / pre1_group][hidden1]) is added to
  * the first layer's pre-activation of every row n as pre1[n / pre1_group]: the MAPPO critic's
  * first layer over local_w || global (multi_env.py:566-573) is W_local x_w + (W_global g_env + b1),
  * with the global block computed once per env (pre1_group = agents). */
+int msc_mlp3_w3_layout(int32_t out_dim);
 int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
                           int32_t out_dim, const float* w1p, const float* b1, const float* w2p, const float* b2,
                           const float* w3p, const float* b3, float* out, const float* pre1, int32_t pre1_group,

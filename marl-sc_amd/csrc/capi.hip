@@ -783,6 +783,8 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
   return 0;
 }
 
+int msc_mlp3_w3_layout(int32_t out_dim) { return out_dim >= 1 && out_dim <= 32 ? (mlp3_valu_outputs(out_dim) > 0 ? 1 : 0) : -1; }
+
 int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
                           int32_t out_dim, const float* w1p, const float* b1, const float* w2p, const float* b2,
                           const float* w3p, const float* b3, float* out, const float* pre1, int32_t pre1_group,

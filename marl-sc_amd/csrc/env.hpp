@@ -134,6 +134,7 @@ hipError_t launch_gae(const float* r, const float* v, const float* nv, const uin
                       int64_t n, int32_t T, float gamma, float lam, float* adv, float* tgt, int32_t n_groups,
                       double* stats, hipStream_t st);
 hipError_t launch_adv_normalize(float* adv, int64_t n, int32_t n_groups, const double* stats, hipStream_t st);
+int mlp3_valu_outputs(int KO);
 hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, int KO, const float* w1p, const float* b1,
                             const float* w2p, const float* b2, const float* w3p, const float* b3, float* out,
                             const float* pre1, int grp, hipStream_t st);

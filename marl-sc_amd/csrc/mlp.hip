@@ -33,18 +33,29 @@ __device__ __forceinline__ int mfma_row(int r, int h) { return (r & 3) + 8 * (r 
 // Weight fragments are software-pipelined one step ahead (the loads of step s + 1 are issued before
 // the MFMAs of step s): with one wave per SIMD nothing else hides an L2 round trip, and a wait on
 // each step's own loads cost ~35 % of the MFMA time.
-template <int NT1, int NT2, int P, int WPE>
+// VKO > 0: the output layer (KO <= VKO <= 8 outputs) on the VALU instead of a 32-row MFMA tile
+// padded from KO rows (an output MFMA tile of 5 actions is 84 % padding: 128 of the actor's 1,312
+// MFMAs). Each lane accumulates its half of the hidden units into VKO f32 sums with the weights read
+// from LDS (all lanes of a half read the same 32 bytes: broadcast), and the two halves are added
+// with one lane exchange. The packed w3 is then [NT2 * 16][2][8] floats (zero past KO).
+template <int NT1, int NT2, int P, int WPE, int VKO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mlp3_relu_kernel(
     const float* __restrict__ x, int64_t n, int L, int KS1, const float4* __restrict__ w1p, const float* __restrict__ b1,
     const float4* __restrict__ w2p, const float* __restrict__ b2, const float4* __restrict__ w3p,
     const float* __restrict__ b3, int KO, float* __restrict__ out, const float* __restrict__ pre1, int grp, int prio) {
   static_assert(NT2 % P == 0, "layer-2 passes");
+  static_assert(VKO >= 0 && VKO <= 8, "VALU output layer: at most 8 outputs");
   constexpr int S4 = NT1 * 4;  // layer-2 k steps of 4 MFMAs (2 hidden units each)
   // the policy forward is on the rollout's critical path (step t + 1 needs its actions), the
   // pipelined demand kernel of step t + 1 (priorities 1-2) is not: issue ahead of it
   if (prio) __builtin_amdgcn_s_setprio(3);
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ float4 w3s[VKO > 0 ? NT2 * 16 * 2 * 2 : 1];  // [s][h][8 floats]
+  if constexpr (VKO > 0) {
+    for (int i = threadIdx.x; i < NT2 * 16 * 2 * 2; i += blockDim.x) w3s[i] = w3p[i];
+    __syncthreads();
+  }
   if (tile * 32 >= n) return;  // wave-uniform (no block-level synchronisation below)
   const int64_t j = tile * 32 + (lane & 31);
   const bool jv = j < n;
@@ -116,10 +127,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   // layers 2 and 3 in passes of P output tiles: the output layer accumulates each pass's slice of
   // the hidden units as soon as it is final, so H2 is never held whole
   mlp_f32x16 a3;
+  float o3[VKO > 0 ? VKO : 1];
+  if constexpr (VKO > 0) {
 #pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const int row = mfma_row(r, h);
-    a3[r] = row < KO ? b3[row] : 0.0f;
+    for (int a = 0; a < VKO; a++) o3[a] = (h == 0 && a < KO) ? b3[a] : 0.0f;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int row = mfma_row(r, h);
+      a3[r] = row < KO ? b3[row] : 0.0f;
+    }
   }
   float4 w[2][P];  // [step parity][tile]: the fragments of step s4 and s4 + 1
 #pragma unroll
@@ -160,6 +177,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         }
       }
     }
+    if constexpr (VKO > 0) {  // layer 3 on the VALU: o[a] += W3[a][hidden] relu(h2) over this lane's half
+#pragma unroll
+      for (int q = 0; q < P; q++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const float hv = fmaxf(a2[q][r], 0.0f);
+          const int sidx = ((p * P + q) * 16 + r) * 2 + h;
+          const float4 wa = w3s[sidx * 2];
+          const float wv[8] = {wa.x, wa.y, wa.z, wa.w, 0.f, 0.f, 0.f, 0.f};
+          float wh[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (VKO > 4) {
+            const float4 wb = w3s[sidx * 2 + 1];
+            wh[0] = wb.x, wh[1] = wb.y, wh[2] = wb.z, wh[3] = wb.w;
+          }
+#pragma unroll
+          for (int a = 0; a < VKO; a++) o3[a] = fmaf(a < 4 ? wv[a] : wh[a - 4], hv, o3[a]);
+        }
+      continue;
+    }
     // layer 3 on this pass's slice: the fragments of tile q + 1 are in flight during tile q
     float4 w3[2][4];
 #pragma unroll
@@ -181,7 +217,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       }
     }
   }
-  if (jv) {
+  if constexpr (VKO > 0) {
+#pragma unroll
+    for (int a = 0; a < VKO; a++) o3[a] += __shfl_xor(o3[a], 32);  // the other half's hidden units
+    if (jv && h == 0) {
+#pragma unroll
+      for (int a = 0; a < VKO; a++)
+        if (a < KO) out[j * KO + a] = o3[a];
+    }
+  } else if (jv) {
 #pragma unroll
     for (int r = 0; r < 16; r++) {
       const int row = mfma_row(r, h);
@@ -208,6 +252,17 @@ static int mlp_prio() {
   return v;
 }
 
+// outputs of the VALU output layer for KO outputs (0: MFMA output layer); MSC_MLP_V3=0 forces the
+// MFMA one (A/B). The host's weight packing must agree: msc_mlp3_w3_layout reports it.
+int mlp3_valu_outputs(int KO) {
+  static const int off = [] {
+    const char* e = getenv("MSC_MLP_V3");
+    return (e && atoi(e) == 0) ? 1 : 0;
+  }();
+  if (off || KO > 8) return 0;
+  return KO <= 2 ? KO : KO <= 4 ? 4 : KO == 5 ? 5 : 8;
+}
+
 hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, int KO, const float* w1p, const float* b1,
                             const float* w2p, const float* b2, const float* w3p, const float* b3, float* out,
                             const float* pre1, int grp, hipStream_t st) {
@@ -218,20 +273,32 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
   const float4* w1 = reinterpret_cast<const float4*>(w1p);
   const float4* w2 = reinterpret_cast<const float4*>(w2p);
   const float4* w3 = reinterpret_cast<const float4*>(w3p);
-#define MSC_MLP_LAUNCH(NT1, NT2, P, WPE)                                                                          \
-  hipLaunchKernelGGL((mlp3_relu_kernel<NT1, NT2, P, WPE>), grid, block, 0, st, x, n, L, KS1, w1, b1, w2, b2, w3, b3, \
-                     KO, out, pre1, grp, mlp_prio())
+#define MSC_MLP_LAUNCH(NT1, NT2, P, WPE, VKO)                                                                          \
+  hipLaunchKernelGGL((mlp3_relu_kernel<NT1, NT2, P, WPE, VKO>), grid, block, 0, st, x, n, L, KS1, w1, b1, w2, b2, w3, \
+                     b3, KO, out, pre1, grp, mlp_prio())
+  // the output layer on the VALU for KO <= 8 (VKO = 1, 2, 4, 5 or 8: the next supported count >= KO)
+  const int vko = mlp3_valu_outputs(KO);
+#define MSC_MLP_VKO(NT1, NT2, P, WPE)                                 \
+  switch (vko) {                                                      \
+    case 1: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 1); break;               \
+    case 2: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 2); break;               \
+    case 4: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 4); break;               \
+    case 5: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 5); break;               \
+    case 8: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 8); break;               \
+    default: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 0); break;              \
+  }
   if (H1 == 256 && H2 == 256) {
-    if (mlp_p8() == 8) MSC_MLP_LAUNCH(8, 8, 8, 1);
-    else if (mlp_p8() == 4) MSC_MLP_LAUNCH(8, 8, 4, 2);
-    else MSC_MLP_LAUNCH(8, 8, 2, 2);
+    if (mlp_p8() == 8) MSC_MLP_VKO(8, 8, 8, 1)
+    else if (mlp_p8() == 4) MSC_MLP_VKO(8, 8, 4, 2)
+    else MSC_MLP_VKO(8, 8, 2, 2)
   } else if (H1 == 128 && H2 == 128) {
-    MSC_MLP_LAUNCH(4, 4, 4, 2);
+    MSC_MLP_VKO(4, 4, 4, 2)
   } else if (H1 == 64 && H2 == 64) {
-    MSC_MLP_LAUNCH(2, 2, 2, 4);
+    MSC_MLP_VKO(2, 2, 2, 4)
   } else {
     return hipErrorInvalidValue;
   }
+#undef MSC_MLP_VKO
 #undef MSC_MLP_LAUNCH
   return hipGetLastError();
 }

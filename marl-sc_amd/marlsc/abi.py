@@ -114,6 +114,7 @@ def lib() -> C.CDLL:
     L.msc_adv_normalize_grouped.argtypes = [vp, C.c_int64, C.c_int32, vp, vp]
     L.msc_env_set_episode_counters.argtypes = [vp, vp]
     L.msc_gaussian_sample.argtypes = [vp, vp, C.c_int32, C.c_float, vp, C.c_int64, C.c_int32, vp, vp, vp, vp]
+    L.msc_mlp3_w3_layout.argtypes = [C.c_int32]
     L.msc_mlp3_relu_forward.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp, vp, vp,
                                         vp, vp, vp, C.c_int32, vp]
     L.msc_seedseq_u32.argtypes = [P(C.c_uint32), C.c_int32]
@@ -135,5 +136,5 @@ def check(rc: int) -> None:
 EXPORTED_SYMBOLS = [
     "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_timing", "msc_env_read_timing", "msc_env_obs_flat",
     "msc_env_read_state", "msc_env_state_bytes", "msc_env_save_state", "msc_env_load_state", "msc_env_check",
-    "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_relu_forward", "msc_seedseq_u32", "msc_last_error", "msc_abi_version",
+    "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_w3_layout", "msc_mlp3_relu_forward", "msc_seedseq_u32", "msc_last_error", "msc_abi_version",
 ]

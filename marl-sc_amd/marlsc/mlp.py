@@ -34,8 +34,8 @@ def _rho(r: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     return (r & 3) + 8 * (r >> 2) + 4 * h
 
 
-def _index_maps(L: int, H1: int, H2: int, KO: int, device) -> Tuple[torch.Tensor, ...]:
-    key = (L, H1, H2, KO, str(device))
+def _index_maps(L: int, H1: int, H2: int, KO: int, device, w3_layout: int) -> Tuple[torch.Tensor, ...]:
+    key = (L, H1, H2, KO, str(device), w3_layout)
     if key in _IDX:
         return _IDX[key]
     KS1 = (L + 1) // 2
@@ -55,21 +55,39 @@ def _index_maps(L: int, H1: int, H2: int, KO: int, device) -> Tuple[torch.Tensor
     hh = h[None, None, :, None]
     cc = c[None, None, :, None]
     i2 = ((t2 * 32 + cc) * H1 + (s // 16) * 32 + _rho(s % 16, hh)).reshape(-1)
-    # w3p[q][lane][i] = W3[c][32 (q // 4) + rho(4 (q % 4) + i, h)]  (0 for output rows >= KO)
-    q = torch.arange((H2 // 32) * 4, device=device)[:, None, None]
-    r = (q % 4) * 4 + torch.arange(4, device=device)[None, None, :]
-    c3, h3 = c[None, :, None], h[None, :, None]
-    i3 = (c3.clamp(max=KO - 1) * H2 + (q // 4) * 32 + _rho(r, h3)).reshape(-1)
-    v3 = (c3 < KO).expand((H2 // 32) * 4, 64, 4).reshape(-1)
+    if w3_layout == 0:
+        # w3p[q][lane][i] = W3[c][32 (q // 4) + rho(4 (q % 4) + i, h)]  (0 for output rows >= KO)
+        q = torch.arange((H2 // 32) * 4, device=device)[:, None, None]
+        r = (q % 4) * 4 + torch.arange(4, device=device)[None, None, :]
+        c3, h3 = c[None, :, None], h[None, :, None]
+        i3 = (c3.clamp(max=KO - 1) * H2 + (q // 4) * 32 + _rho(r, h3)).reshape(-1)
+        v3 = (c3 < KO).expand((H2 // 32) * 4, 64, 4).reshape(-1)
+    else:
+        # VALU output layer: w3p[s][h][a] = W3[a][32 (s // 16) + rho(s % 16, h)]  (0 for a >= KO)
+        sv = torch.arange((H2 // 32) * 16, device=device)[:, None, None]
+        hv = torch.arange(2, device=device)[None, :, None]
+        av = torch.arange(8, device=device)[None, None, :]
+        i3 = (av.clamp(max=KO - 1) * H2 + (sv // 16) * 32 + _rho(sv % 16, hv)).reshape(-1)
+        v3 = (av < KO).expand((H2 // 32) * 16, 2, 8).reshape(-1)
     _IDX[key] = (i1, v1, i2, i3, v3)
     return _IDX[key]
 
 
-def pack_mlp3(w1: torch.Tensor, w2: torch.Tensor, w3: torch.Tensor):
-    """Torch Linear weights ([H1, L], [H2, H1], [KO, H2]) -> (w1p, w2p, w3p) fragment order."""
+def w3_layout(out_dim: int) -> int:
+    """Packed layout of the output layer the kernel uses for out_dim outputs (msc_mlp3_w3_layout):
+    0 = MFMA fragments [H2/8][64][4], 1 = VALU rows [H2/2][2][8]."""
+    v = abi.lib().msc_mlp3_w3_layout(int(out_dim))
+    if v < 0:
+        raise ValueError(f"the fused MLP supports 1..{MAX_OUT} outputs, not {out_dim}")
+    return v
+
+
+def pack_mlp3(w1: torch.Tensor, w2: torch.Tensor, w3: torch.Tensor, layout: Optional[int] = None):
+    """Torch Linear weights ([H1, L], [H2, H1], [KO, H2]) -> (w1p, w2p, w3p) fragment order;
+    layout: the output layer's (w3_layout(KO) when None)."""
     H1, L = w1.shape
     H2, KO = w2.shape[0], w3.shape[0]
-    i1, v1, i2, i3, v3 = _index_maps(L, H1, H2, KO, w1.device)
+    i1, v1, i2, i3, v3 = _index_maps(L, H1, H2, KO, w1.device, w3_layout(KO) if layout is None else layout)
     zero = torch.zeros((), device=w1.device, dtype=torch.float32)
     w1p = torch.where(v1, w1.detach().float().reshape(-1)[i1], zero)
     w2p = w2.detach().float().reshape(-1)[i2]

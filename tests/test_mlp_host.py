@@ -29,16 +29,15 @@ def _regs(tile, r):
     return np.array([tile[_rho(r, lane >> 5), lane & 31] for lane in range(64)])
 
 
-def _emulate(mlp, x):
+def _emulate(mlp, x, layout=0):
     l1, _, l2, _, l3 = list(mlp)
     H1, L = l1.weight.shape
     H2, KO = l2.weight.shape[0], l3.weight.shape[0]
     KS1 = (L + 1) // 2
     M4 = (KS1 + 3) // 4
-    w1p, w2p, w3p = (t.double().numpy() for t in pack_mlp3(l1.weight, l2.weight, l3.weight))
+    w1p, w2p, w3p = (t.double().numpy() for t in pack_mlp3(l1.weight, l2.weight, l3.weight, layout))
     w1p = w1p.reshape(H1 // 32, M4, 64, 4)
     w2p = w2p.reshape(H2 // 32, H1 // 8, 64, 4)
-    w3p = w3p.reshape(H2 // 8, 64, 4)
     b1, b2, b3 = (m.bias.detach().double().numpy() for m in (l1, l2, l3))
     n = x.shape[0]
     assert n == 32  # one wave
@@ -56,6 +55,15 @@ def _emulate(mlp, x):
         for s in range((H1 // 32) * 16):
             d = _mfma(w2p[t2, s // 4, :, s % 4], _regs(h1[s // 16], s % 16), d)
         h2.append(np.maximum(d + b2[t2 * 32:(t2 + 1) * 32, None], 0))
+    if layout == 1:  # VALU output layer: lane half h sums its rows rho(r, h) of every tile
+        w3v = w3p.reshape((H2 // 32) * 16, 2, 8)
+        o = np.zeros((64, 8))
+        for s in range((H2 // 32) * 16):
+            hv = _regs(h2[s // 16], s % 16)
+            for lane in range(64):
+                o[lane] += w3v[s, lane >> 5] * hv[lane]
+        return o[:32, :KO] + o[32:, :KO] + b3[None, :]
+    w3p = w3p.reshape(H2 // 8, 64, 4)
     d = np.zeros((32, 32))
     for q in range((H2 // 32) * 4):
         for i in range(4):
@@ -63,13 +71,14 @@ def _emulate(mlp, x):
     return (d[:KO] + b3[:, None]).T
 
 
+@pytest.mark.parametrize("layout", [0, 1])
 @pytest.mark.parametrize("L,H,KO", [(34, 64, 5), (7, 64, 1), (42, 128, 3)])
-def test_packed_fragments_reproduce_the_mlp(L, H, KO):
+def test_packed_fragments_reproduce_the_mlp(L, H, KO, layout):
     torch.manual_seed(L * H + KO)
     mlp = MLP(L, KO, {"hidden_sizes": [H, H]})
     assert fusable(list(mlp))
     x = torch.randn(32, L, dtype=torch.float64)
-    got = _emulate(mlp, x.numpy())
+    got = _emulate(mlp, x.numpy(), layout)
     ref = mlp.double()(x).detach().numpy()
     np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
 
@@ -102,3 +111,11 @@ def test_mlp3_abi_rejects_bad_arguments_before_any_launch():
     q = C.c_void_p(20)  # misaligned bias
     assert f(p, 8, 34, 64, 64, 5, p, q, p, p, p, p, p, None, 1, None) == -1
     assert b"aligned" in L.msc_last_error()
+
+
+def test_output_layer_layout_rule():
+    from marlsc.mlp import w3_layout
+    assert [w3_layout(k) for k in (1, 5, 8)] == [1, 1, 1]  # VALU output layer up to 8 outputs
+    assert [w3_layout(k) for k in (9, 32)] == [0, 0]       # MFMA tile beyond
+    with pytest.raises(ValueError):
+        w3_layout(33)
