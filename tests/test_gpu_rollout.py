@@ -149,6 +149,23 @@ def test_fused_mlp3_kernel_matches_torch_layers(L, H, KO, n):
     torch.testing.assert_close(got, ref, rtol=2e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("W,L", [(8, 34), (16, 42), (3, 13)])
+def test_fused_mappo_critic_matches_split_layers(W, L):
+    # the MAPPO critic over local_w || global through the fused kernel (per-env global block as the
+    # first layer's pre1 term, group = W agents) against the same split MLP in torch layers
+    from marlsc.rollout import MLP, split_global_mlp
+    torch.manual_seed(W * L)
+    critic = MLP(L * (1 + W), 1, {"hidden_sizes": [64, 64]}).cuda()
+    x = torch.randn(777, W, L, device="cuda")
+    with torch.no_grad():
+        fused = split_global_mlp(critic, x)
+    with torch.enable_grad():
+        ref = split_global_mlp(critic, x).detach()
+        full = critic(torch.cat([x, x.reshape(777, 1, W * L).expand(777, W, W * L)], dim=-1)).detach()
+    torch.testing.assert_close(fused, ref, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(fused, full, rtol=2e-5, atol=2e-5)
+
+
 def test_gaussian_sample_kernel_matches_torch_formula():
     # msc_gaussian_sample against the TorchDiagGaussian restatement in torch fp32
     import math
