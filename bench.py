@@ -74,6 +74,117 @@ def _mlp_traffic(tj: Path, key: str):
     return json.loads(tj.read_text()).get("mlp3_relu_kernel", {}).get(key, {}).get("traffic")
 
 
+def bench_obs_stats(cfg, meta, n_episodes: int = 2):
+    """meanstd_custom statistics (obs_stats.py:11-90) from a short random-policy run on the GPU env
+    (the reference uses 100 episodes; the values only set the normalisation constants, not the work)."""
+    from marlsc.ppo import compute_obs_statistics
+    from marlsc.seeding import SeedManager
+    return compute_obs_statistics(cfg, SeedManager(42), "meanstd_custom", n_episodes=n_episodes, env_meta=meta)
+
+
+def time_env(env, pool, steps: int, warmup: int, world: int):
+    """warmup untimed steps, then `steps` timed ones (barrier + synchronize on both sides); then a
+    timing pass of min(steps, 50) steps with the library's per-launch HIP events."""
+    import torch
+    import torch.distributed as dist
+    for i in range(warmup):
+        env.step(pool[i % len(pool)])
+    env.check()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        env.step(pool[i % len(pool)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    env.check()
+    kp = min(steps, 50)
+    env.set_timing(kp)
+    for i in range(kp):
+        env.step(pool[i % len(pool)])
+    tm = env.read_timing()
+    tm.update(env.read_timing_ea())
+    env.set_timing(0)
+    env.check()
+    return dt, tm
+
+
+def time_rollout(envs, module, T: int, world: int, seed: int, warm: int = 1, reps: int = 1):
+    """Seconds per rollout of T steps (RolloutCollector.collect) after `warm` untimed ones."""
+    import torch
+    import torch.distributed as dist
+    from marlsc.rollout import RolloutCollector
+    col = RolloutCollector(envs, module, T, seed=seed)
+    for _ in range(warm):
+        col.collect()  # warm-up (GEMM heuristics, allocator; episode-ahead demand reaches steady state)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        col.collect()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    for x in (envs if isinstance(envs, list) else [envs]):
+        x.check()
+    return (time.perf_counter() - t0) / reps
+
+
+def c2_line(args, rank: int):
+    """BASELINE configs[1]: 8 x 64 x 5, 4,096 envs on one GPU, IPPO rollout (the reference's
+    config_files/algorithms/ippo.yaml: actor / critic [256], critic on local obs, meanstd_custom)."""
+    import torch
+    import yaml
+    from marlsc import make_synthetic_env_config
+    from marlsc.rollout import ActorCritic, RolloutConfig
+    from marlsc.seeding import default_train_seed
+    from marlsc.spec import EnvSpec
+    from marlsc.vec_env import VecInventoryEnv
+    algo = yaml.safe_load(open(REPO / "config_files/algorithms/ippo.yaml"))
+    norm = algo["algorithm"]["algorithm_specific"]["obs_normalization"]
+    cfg = make_synthetic_env_config(8, 64, 5)
+    meta = {"include_warehouse_id": True, "obs_normalization": norm}
+    meta["obs_stats"] = bench_obs_stats(cfg, meta)
+    spec = EnvSpec.from_config(cfg, meta)
+    E = args.c2_envs
+    env = VecInventoryEnv(None, E, spec=spec, device=torch.cuda.current_device(), base_seed=default_train_seed(42))
+    g = torch.Generator(device="cuda").manual_seed(99)
+    pool = [torch.rand((E, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
+    env.reset()
+    T = spec.episode_length
+    steps = max(args.steps, 5 * T)
+    warm = 3 * T  # episode 0 of the episode-ahead snapshot draws per step; later ones read slots
+    dt, tm = time_env(env, pool, steps, warm, 1)
+    rc = RolloutConfig.from_algorithm_config(algo)
+    torch.manual_seed(0)
+    module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
+    t_roll = time_rollout(env, module, T, 1, seed=rank, warm=2, reps=2) if args.rollout_T > 0 else 0.0
+    a_h, c_h = rc.actor["hidden_sizes"], rc.critic["hidden_sizes"]
+    out = {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x {spec.K} SKUs "
+                       f"(BASELINE configs[1])",
+           "value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "ms_per_step": round(dt / steps * 1e3, 4),
+           "steps": steps, "warmup": warm, "obs_normalization": norm,
+           "demand": (f"episode-ahead: whole episodes drawn on a side stream, {tm['slots']} slots per env"
+                      if tm["slots"] else "per step (pipelined)"),
+           "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
+                          "demand_ea_kernel_per_episode": round(tm["ea_ms"], 4) if tm["n_ea"] else None,
+                          "demand_per_step": round(tm["demand_ms"], 4) if tm["n_demand"] else None}}
+    if args.rollout_T > 0:
+        out["rollout"] = {"value": round(E * spec.W * T / t_roll, 1), "unit": "agent-steps/s",
+                          "ms_per_step": round(t_roll / T * 1e3, 4), "T": T,
+                          "policy": f"IPPO (config_files/algorithms/ippo.yaml): actor {spec.local_obs_dim}-"
+                                    f"{'-'.join(map(str, a_h))}-{spec.K}, critic {spec.local_obs_dim}-"
+                                    f"{'-'.join(map(str, c_h))}-1 on local obs, fp32, parameter sharing",
+                          "includes": "env step, actor + critic forward, Gaussian sampling, buffer writes, truncation "
+                                      "bootstrap, GAE kernel, adv-norm statistics + normalise"}
+    env.close()
+    return out
+
+
 def cpu_baseline(spec, seconds: float):
     """The C oracle on the host's cores (<= 16 threads), plus a 1-core figure."""
     out = _cpu_rate(spec, seconds, max(1, min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
@@ -122,6 +233,9 @@ def main():
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "traffic.json"))
     ap.add_argument("--rollout-T", type=int, default=100,
                     help="steps of the MAPPO rollout line (0 = skip): env + actor/critic forward + buffers + GAE")
+    ap.add_argument("--c2-envs", type=int, default=4096, help="envs of the configs[1] line (0 = skip it)")
+    ap.add_argument("--obs-norm", choices=("meanstd_custom", "off"), default="meanstd_custom",
+                    help="observation normalisation of the headline env (the reference MAPPO config's is meanstd_custom)")
     ap.add_argument("--rollout-lanes", type=int, default=int(os.environ.get("MSC_ROLLOUT_LANES", "1")),
                     help="env handles the rollout's envs are split into, each stepping on its own HIP stream so one "
                          "lane's env kernels overlap another's policy GEMMs (1 = one handle, one stream)")
@@ -164,6 +278,9 @@ def main():
         meta["demand_trace"] = make_synthetic_trace(256, 5, 300, orders_per_step=(200, 1000), seed=0)
     else:
         cfg = make_synthetic_env_config(args.agents, args.regions, args.skus)
+    if args.obs_norm != "off":
+        meta["obs_normalization"] = args.obs_norm
+        meta["obs_stats"] = bench_obs_stats(cfg, dict(meta))
     spec = EnvSpec.from_config(cfg, meta)
     E = args.envs if args.envs is not None else (8192 if args.config == "c5" else 32768)
     dev = torch.cuda.current_device()
@@ -171,34 +288,13 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
     pool = [torch.rand((E, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
     env.reset()
-    for i in range(args.warmup):
-        env.step(pool[i % 8])
-    env.check()
 
     K = args.steps
     # (1) the timed run: the production step path (demand of step t+1 pipelined on the library's
-    #     side stream behind the step kernel of step t, see msc_env_step)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(K):
-        env.step(pool[i % 8])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    env.check()
-    # (2) per-launch device durations for the roofline, in the production (pipelined) regime:
-    #     the library brackets each demand launch and each step launch (step_a/b/c) with HIP events
-    #     on the stream it runs on (side stream for pipelined demand), msc_env_set_timing
-    KP = min(K, 50)
-    env.set_timing(KP)
-    for i in range(KP):
-        env.step(pool[i % 8])
-    tm = env.read_timing()
-    env.set_timing(0)
-    env.check()
+    #     side stream behind the step kernel of step t, see msc_env_step), then (2) per-launch device
+    #     durations for the roofline in the same regime: the library brackets each demand launch and
+    #     each step launch (step_a/b/c) with HIP events on the stream it runs on (msc_env_set_timing)
+    dt, tm = time_env(env, pool, K, args.warmup, world)
     t_demand, t_step = tm["demand_ms"] / 1e3, tm["step_ms"] / 1e3
     # (3) MAPPO rollout (configs[2]): env step + actor/critic forward + sampling + buffer writes +
     #     GAE kernel + adv-norm statistics all-reduce, T steps per rollout
@@ -220,19 +316,7 @@ def main():
             for x in renv:
                 x.set_pipelining(os.environ.get("MSC_ROLLOUT_PIPELINE", "1") != "0")
                 x.reset()
-        col = RolloutCollector(renv, module, args.rollout_T, seed=rank)
-        col.collect()  # warm-up (GEMM heuristics, allocator)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        col.collect()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t_roll = time.perf_counter() - t0
-        for x in (renv if isinstance(renv, list) else [renv]):
-            x.check()
+        t_roll = time_rollout(renv, module, args.rollout_T, world, seed=rank)
     # (4) the HBM-bound kernel of the rollout: msc_gae (GAE reverse scan + advantage statistics) over
     #     one MAPPO rollout's [T, E * W] sequences, timed alone with events on its stream
     gae_line = None
@@ -294,6 +378,10 @@ def main():
                         "shape": f"actor {spec.local_obs_dim}-{H1}-{H2}-{spec.K} over N={N} rows (E x W of one rollout step), "
                                  f"f32 MFMA, timed alone"}
             del xg, yo
+    c2 = None
+    if world == 1 and args.c2_envs > 0 and args.config == "c3":
+        env.close()
+        c2 = c2_line(args, rank)
     tt = torch.tensor([dt, t_roll], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -357,7 +445,7 @@ def main():
                                                         else "(BASELINE configs[4], empirical trace)"),
                        "n_envs_per_gpu": E, "agents": spec.W, "regions": spec.R, "skus": spec.K,
                        "episode_length": spec.episode_length, "obs_dim_local": spec.local_obs_dim,
-                       "parallelism": f"env-shard x{world}"},
+                       "obs_normalization": meta.get("obs_normalization", "off"), "parallelism": f"env-shard x{world}"},
             "kernels_ms": {DEMAND_KERNEL: round(t_demand * 1e3, 4), "step_kernels": round(t_step * 1e3, 4)},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -377,10 +465,13 @@ def main():
                 "value": round(E * world * spec.W * args.rollout_T / t_roll, 1), "unit": "agent-steps/s",
                 "ms_per_step": round(t_roll / args.rollout_T * 1e3, 4), "T": args.rollout_T,
                 "policy": f"MAPPO (config_files/algorithms/mappo.yaml): actor {spec.local_obs_dim}-256-256-{spec.K} (fused f32-MFMA kernel), "
-                          f"critic {spec.local_obs_dim * (1 + spec.W)}-64-64-1, fp32, parameter sharing",
+                          f"critic {spec.local_obs_dim * (1 + spec.W)}-64-64-1, fp32, parameter sharing, "
+                          f"obs {meta.get('obs_normalization', 'off')}",
                 "lanes": max(1, args.rollout_lanes),
                 "includes": "env step (envs split into `lanes` handles on their own HIP streams), actor forward, MAPPO critic on local||global (first layer split: global block once per env), Gaussian sampling, "
                             "buffer writes, truncation bootstrap, GAE kernel, adv-norm all-reduce + normalise"}
+        if c2 is not None:
+            out["c2"] = c2
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
         print(json.dumps(out))

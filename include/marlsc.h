@@ -214,6 +214,14 @@ int msc_env_set_timing(msc_env* env, int32_t max_steps);
  * the recorded events). */
 int msc_env_read_timing(msc_env* env, double* demand_ms, double* step_ms, int64_t* n_demand,
                         int64_t* n_step);
+/* Episode-ahead demand (few envs per GPU: E <= 8192 by default, MSC_EA=0|1 forces it): while
+ * every env sits at the same timestep, the Poisson orders of whole future episodes are drawn on a
+ * library-owned stream (an episode's demand depends only on its SeedSequence([root, counter]) seed,
+ * src/utils/seed_manager.py:100-120, never on actions); each env step then reads its episode's
+ * slot. Results are identical with and without it. Mean device duration of the episode generation
+ * launches timed since msc_env_set_timing (one launch = one episode of every env in steady state),
+ * their count, the slots per env (0: EA off) and whether the current episode reads a slot. */
+int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* slots, int32_t* active);
 
 /* Flat per-agent observation of the reference [E][W][L*(1+W)] = local_w || local_0..local_{W-1},
  * from the compact obs [E][W][L]. */
@@ -294,11 +302,22 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
  * the first layer's pre-activation of every row n as pre1[n / pre1_group]: the MAPPO critic's
  * first layer over local_w || global (multi_env.py:566-573) is W_local x_w + (W_global g_env + b1),
  * with the global block computed once per env (pre1_group = agents). */
+/* hidden1, hidden2 in {64, 128, 256, 512} (equal or not). */
 int msc_mlp3_w3_layout(int32_t out_dim);
 int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
                           int32_t out_dim, const float* w1p, const float* b1, const float* w2p, const float* b2,
                           const float* w3p, const float* b3, float* out, const float* pre1, int32_t pre1_group,
                           msc_stream_t stream);
+
+/* The one-hidden-layer form out = W3 relu(W1 x + b1) + b3 (MLPArchitecture.build with
+ * hidden_sizes [H]: the reference IPPO actor / critic [256], config_files/algorithms/ippo.yaml:46,52,
+ * and the test configs' [128] / [1024] heads), hidden a multiple of 32 up to 1024, out_dim <= 32:
+ * the hidden layer is produced 256 units at a time and folded into the outputs in registers.
+ * w1p as msc_mlp3_relu_forward's (hidden1 = hidden), w3p as its output layer with hidden2 = hidden
+ * (layout by msc_mlp3_w3_layout(out_dim)); pre1 / pre1_group as there. */
+int msc_mlp2_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden, int32_t out_dim,
+                          const float* w1p, const float* b1, const float* w3p, const float* b3, float* out,
+                          const float* pre1, int32_t pre1_group, msc_stream_t stream);
 
 /* Utility: SeedSequence(words).generate_state(1, uint32)[0] (numpy-compatible), on the host. */
 uint32_t msc_seedseq_u32(const uint32_t* words, int32_t n_words);

@@ -149,24 +149,10 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
   __syncthreads();  // tables
 
   // this env's order list: record (n, v) at base + n * nstep + v * vstep (uint4 units)
-  int n_orders = 0;
-  int64_t base = 0, nstep, vstep;
-  if (c.demand_type == MSC_DEMAND_EMPIRICAL) {
-    if (ev) {
-      const int64_t row = s.emp_start[e] + (s.t[e] % c.T);
-      const int64_t off = c.tr_off[row];
-      n_orders = (int)(c.tr_off[row + 1] - off);
-      base = off * NVR;
-    }
-    nstep = NVR;
-    vstep = 1;
-  } else {
-    n_orders = ev ? s.n_orders[e] : 0;
-    base = ev ? e : 0;
-    nstep = (int64_t)NVR * E;
-    vstep = E;
-  }
-  const MSC_GLOBAL uint4* src = gp(c.demand_type == MSC_DEMAND_EMPIRICAL ? c.tr_rec : s.orders);
+  const OrderSrc osrc = order_src<NVR>(c, s, io, ev ? e : 0);
+  const int n_orders = ev ? osrc.n : 0;
+  const int64_t base = ev ? osrc.base : 0, nstep = osrc.nstep, vstep = osrc.vstep;
+  const MSC_GLOBAL uint4* src = gp(osrc.src);
   if (dbg && ev && jl == 0 && info.n_orders) info.n_orders[e] = n_orders;
   int wmax = n_orders;  // orders of the wave's busiest env
 #pragma unroll

@@ -1,0 +1,360 @@
+// alloc_scan.hip -- phase B of InventoryEnvironment.step for few envs per GPU (BASELINE configs[1]:
+// 4,096 envs): the greedy allocation (GreedyDemandAllocator.allocate, demand_allocator.py:118-217)
+// as a prefix scan over the cost ranking, one env per wave.
+//
+// Why a scan. For one order with demand d_s, the reference walks the warehouses in ascending cost
+// order (argsort of of[w, r] + ov[w, r] * (d . sku_weights), :168-173) and takes
+// fill = min(remaining, inventory) from each (:186), skipping warehouses with nothing to give and
+// stopping after max_splits + 1 contributing ones (:182). Without that stop the fill of SKU s at
+// the warehouse of rank p is exactly
+//     f_{p,s} = min(inv_{p,s}, max(0, d_s - sum_{q<p} inv_{q,s}))       (inventories >= 0),
+// an exclusive prefix sum over the ranking: no data-dependent loop, and every (SKU, warehouse) pair
+// is independent. With the stop, the fills before the (max_splits+1)-th contributing rank are the
+// same and later ones are zero (a mask over the contributing ranks). The few-env configs have few
+// allocation chains (4,096 at configs[1] vs 32,768 at configs[2]), so the chain length per order,
+// not the issue rate, bounds the step: this kernel spends ~25 vector instructions per order on the
+// chain where the group kernel (step_b_kernel) spends ~340.
+//
+// Thread mapping: one env per wave (4 per block), lane = s * GW + w (SKU s, warehouse w; GW = the
+// warehouse count rounded up to 2 / 4 / 8, K * GW <= 64). Per order:
+//   1. rank (off the chain): the wave first ranks a window of 64 orders, one order per lane (the
+//      W costs and their order, packed as 4-bit ranks rho_w), into LDS;
+//   2. ds_permute moves each lane's inventory to the lane of its warehouse's rank (rank space),
+//   3. a 3-step DPP scan over the GW lanes of a SKU gives the exclusive prefix, the fill is one med3,
+//   4. ds_bpermute brings each fill back to its warehouse's lane, which updates its inventory.
+// Region epilogues (orders are region-major) fold the region into lost sales (shipment share /
+// closest / cost softmax, lost_sales_handler.py:71-210), outbound costs (reward_calculator.py:
+// 139-142: counts x fixed + (shipped . weights) x variable, per region as the reference sums them)
+// and the home-region features (multi_env.py:767-773). Inputs: any order source (order_src: the
+// Poisson step buffer, an episode-ahead slot, the empirical trace).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "env.hpp"
+#include "kcommon.hpp"
+
+namespace msc {
+
+constexpr int SC_WAVES = 4;  // envs (waves) per block
+constexpr int SC_WIN = 64;   // orders ranked per window (one per lane)
+#ifndef MSC_SC_PRIO
+#define MSC_SC_PRIO 3  // s_setprio: the step chain is the critical path next to the demand generator
+#endif
+
+// LDS per wave: the window's order records and their packed ranks, epilogue scratch
+struct ScWaveLds {
+  uint4 rec[SC_WIN];
+  uint2 hdr[SC_WIN];  // {region, rho}
+  int32_t iscr[64];
+  double dscr[64];
+};
+constexpr size_t sc_tab_bytes(int R, int GW) { return (size_t)(R | 1) * GW * 16; }
+constexpr size_t SC_TAB_MAX = 32 * 1024;
+
+// inclusive prefix sum over the GW lanes of each group (p = lane % GW), DPP row shifts inside the
+// 16-lane rows with the lanes whose source belongs to the previous group masked
+template <int GW>
+__device__ __forceinline__ int group_scan(int x, int p) {
+  int v = x;
+  int t = __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);  // row_shr:1
+  v += p >= 1 ? t : 0;
+  if constexpr (GW >= 4) {
+    t = __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += p >= 2 ? t : 0;
+  }
+  if constexpr (GW >= 8) {
+    // row_shr:4 into banks 1 and 3 only (lanes 4-7, 12-15 of a row: p >= 4); others add 0
+    t = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xA, false);
+    v += t;
+  }
+  return v;
+}
+// OR of the 64 / GW groups' GW-bit fields of a ballot
+template <int GW>
+__device__ __forceinline__ uint32_t fold_groups(uint64_t b) {
+#pragma unroll
+  for (int sh = 32; sh >= GW; sh >>= 1) b |= b >> sh;
+  return (uint32_t)b & ((1u << GW) - 1u);
+}
+template <int GW, typename T, typename F>
+__device__ __forceinline__ T sc_group_reduce(T v, F op) {
+  v = op(v, dpp_x<0>(v));
+  if constexpr (GW >= 4) v = op(v, dpp_x<1>(v));
+  if constexpr (GW >= 8) v = op(v, dpp_x<2>(v));
+  return v;
+}
+// numpy add.reduce order of the group's lane values v_0..v_{n-1}, n <= GW <= 8 (sequential)
+template <int GW>
+__device__ __forceinline__ double sc_group_np_sum(double v, int n) {
+  double r = 0.0;
+#pragma unroll
+  for (int j = 0; j < GW; j++) {
+    const double x = __shfl(v, j, GW);
+    r = j < n ? r + x : r;
+  }
+  return r;
+}
+
+__device__ __forceinline__ uint32_t rec_field(const uint4& v, int h) {  // h: compile-time after unrolling
+  const uint32_t w = h < 2 ? v.x : h < 4 ? v.y : h < 6 ? v.z : v.w;
+  return (h & 1) ? (w >> 16) : (w & 0xffffu);
+}
+
+template <int K, int GW>
+__global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+  static_assert(K * GW <= 64 && K <= 6, "lane = s * GW + w; one uint4 per order record");
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  const int W = c.W, R = c.R, WK = W * K;
+  const int64_t E = c.E;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * SC_WAVES + wave;
+  const int sk = lane / GW, w = lane % GW;  // this lane's SKU and warehouse (its rank p in rank space)
+  const bool lv = sk < K && w < W;
+  const msc_step_info info = io.info;
+  const bool dbg = io.has_info != 0;
+  if (MSC_SC_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SC_PRIO);
+
+  extern __shared__ __attribute__((aligned(16))) char sc_lds[];
+  const bool tab = sc_tab_bytes(R, GW) <= SC_TAB_MAX;
+  double2* Ltab = reinterpret_cast<double2*>(sc_lds);  // [w][R | 1] {of, ov}
+  ScWaveLds* Lw = reinterpret_cast<ScWaveLds*>(sc_lds + (tab ? sc_tab_bytes(R, GW) : 0)) + wave;
+  const int RS = R | 1;
+  if (tab) {
+    for (int i = threadIdx.x; i < R * GW; i += blockDim.x) {
+      const int ww = i / R, r = i % R;
+      Ltab[ww * RS + r] = ww < W ? make_double2(c.ofT[r * W + ww], c.ovT[r * W + ww]) : make_double2(0.0, 0.0);
+    }
+  }
+  __syncthreads();  // the only block barrier: waves (envs) are independent from here on
+  if (e >= E) return;
+  auto tab_at = [&](int r, int ww) -> double2 {
+    if (tab) return Ltab[ww * RS + r];
+    const int wc = ww < W ? ww : W - 1;
+    return make_double2(gp(c.ofT)[r * W + wc], gp(c.ovT)[r * W + wc]);
+  };
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  // uniform constants in scalar registers
+  double skw[K];
+#pragma unroll
+  for (int j = 0; j < K; j++) skw[j] = sgpr_d(c.skw[j]);
+  const int lost_type = __builtin_amdgcn_readfirstlane(c.lost_type);
+  const int maxwh = __builtin_amdgcn_readfirstlane(c.max_wh);
+  const bool split = maxwh < W;
+  const double alpha = sgpr_d(c.alpha);
+  const int pps = c.pen_per_sku;
+  const double skw_me = sk < K ? c.skw[sk] : 0.0;
+  const double pen_me = sk < K ? (pps ? c.pen[sk] : c.pen_scalar) : 0.0;
+  const int myhome = w < W ? c.home_of[w] : -1;
+
+  const int64_t gi = (int64_t)(w * K + sk) * E + e;  // this lane's [w*K + s][E] state index
+  int inv = lv ? s.inv[gi] : 0;
+  const int inv0 = inv;
+  int qsr = 0, cnt = 0, u = 0, dsum = 0, lost_cnt = 0;
+  double lost = 0.0, ofix = 0.0, ovar = 0.0, of_me = 0.0, ov_me = 0.0;
+  int inc_h = 0, shh_h = 0;
+  bool home_done = false;
+  int cur = -1;
+
+  const OrderSrc o = order_src<1>(c, s, io, e);
+  const int n = o.n;
+  const MSC_GLOBAL uint4* src = gp(o.src);
+  if (dbg && lane == 0 && info.n_orders) info.n_orders[e] = n;
+
+  // region epilogue: lost sales, outbound cost, home features of region r (uniform)
+  auto epilogue = [&](int r) {
+    const int ug = __shfl(u, sk * GW + GW - 1);  // the SKU's unfulfilled demand (kept by its last rank lane)
+    Lw->iscr[lane] = qsr;
+    if (w == GW - 1) Lw->dscr[sk] = (double)ug;
+    wave_sync();
+    int acc = 0;       // units this warehouse shipped to the region (shipment_quantities[w, r])
+    double wsum = 0.0; // their weight (outbound_shipment_weights[w, r], SKU order: numpy's for K < 8)
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const int q = Lw->iscr[j * GW + w];
+      acc += q;
+      wsum += (double)q * skw[j];
+    }
+    if (lost_cnt > 0) {
+      double wt = 0.0;
+      const int tot = sc_group_reduce<GW>(acc, [](int a, int b) { return a + b; });
+      if (lost_type == MSC_LOST_COST) {  // softmax(-(of * lost_orders + ov * lost_weight) / alpha)
+        double lw = 0.0;                 // unfulfilled[r] . sku_weights
+#pragma unroll
+        for (int j = 0; j < K; j++) lw += Lw->dscr[j] * skw[j];
+        const double lg = w < W ? -(of_me * (double)lost_cnt + ov_me * lw) / alpha : -INFINITY;
+        const double mx = sc_group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
+        const double ex = w < W ? exp(lg - mx) : 0.0;
+        wt = w < W ? ex / sc_group_np_sum<GW>(ex, W) : 0.0;
+      } else if (lost_type == MSC_LOST_SHIPMENT && tot > 0) {
+        wt = acc > 0 ? (double)acc / (double)tot : 0.0;
+      } else {  // closest warehouse (shipment with nothing shipped falls back to it)
+        wt = w == c.closest[r] ? 1.0 : 0.0;
+      }
+      if (wt != 0.0) lost += wt * (double)ug;
+    }
+    ofix += (double)cnt * of_me;
+    ovar += wsum * ov_me;
+    if (r == myhome) {
+      inc_h = dsum;
+      shh_h = qsr;
+      home_done = true;
+    }
+    if (dbg) {
+      if (w == 0 && sk < K) {
+        if (info.demand_per_region) info.demand_per_region[(e * R + r) * K + sk] = dsum;
+        if (info.unfulfilled_demands) info.unfulfilled_demands[(e * R + r) * K + sk] = ug;
+      }
+      if (lane == 0 && info.lost_order_counts) info.lost_order_counts[e * R + r] = lost_cnt;
+      if (lv) {
+        if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] = qsr;
+        if (sk == 0 && info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] = cnt;
+        if (sk == 0 && info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] = acc;
+      }
+    }
+    qsr = cnt = u = dsum = 0;
+    lost_cnt = 0;
+    wave_sync();  // iscr / dscr are rewritten by the next epilogue
+  };
+
+  // order ranks (demand_allocator.py:167-173): 4-bit rank of warehouse w at bits 4w (stable order:
+  // lower index first on equal cost); padding warehouses w >= W keep rank w
+  auto rank_of = [&](const uint4& rv) -> uint32_t {
+    const int rr = (int)(rv.x & 0xffffu);
+    double tw = 0.0;  // order.sku_demands.dot(sku_weights)
+#pragma unroll
+    for (int j = 0; j < K; j++) tw += (double)rec_field(rv, 1 + j) * skw[j];
+    double cst[GW];
+#pragma unroll
+    for (int ww = 0; ww < GW; ww++) {
+      const double2 t = tab_at(rr, ww);
+      cst[ww] = t.x + t.y * tw;
+    }
+    uint32_t rho = 0;
+#pragma unroll
+    for (int a = 0; a < GW; a++)
+#pragma unroll
+      for (int b = a + 1; b < GW; b++)
+        if (b < W) rho += cst[b] < cst[a] ? (1u << (4 * a)) : (1u << (4 * b));
+#pragma unroll
+    for (int ww = 0; ww < GW; ww++)
+      if (ww >= W) rho |= (uint32_t)ww << (4 * ww);
+    return rho;
+  };
+
+  const int fi = sk < K ? 1 + sk : 7;  // this lane's 16-bit field of a record (field 7 is 0: K <= 6)
+  uint4 nxt = lane < n ? gload4(src, o.base + (int64_t)lane * o.nstep) : make_uint4(0u, 0u, 0u, 0u);
+  for (int o0 = 0; o0 < n; o0 += SC_WIN) {
+    const int nw = n - o0 < SC_WIN ? n - o0 : SC_WIN;
+    const uint4 rv = nxt;
+    if (o0 + SC_WIN < n) {  // next window's records in flight while this one is allocated
+      const int oi = o0 + SC_WIN + lane;
+      nxt = oi < n ? gload4(src, o.base + (int64_t)oi * o.nstep) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    const uint32_t rho = lane < nw ? rank_of(rv) : 0u;
+    Lw->rec[lane] = rv;
+    Lw->hdr[lane] = make_uint2(rv.x & 0xffffu, rho);
+    wave_sync();
+    const uint16_t* Lh = reinterpret_cast<const uint16_t*>(Lw->rec);
+    for (int i = 0; i < nw; i++) {
+      const uint2 hd = Lw->hdr[i];
+      const int d = Lh[i * 8 + fi];
+      const int r = __builtin_amdgcn_readfirstlane((int)hd.x);
+      const uint32_t rho_i = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.y);
+      if (r != cur) {  // region boundary (orders are region-major)
+        if (cur >= 0) epilogue(cur);
+        cur = r;
+        const double2 t = tab_at(r, w);
+        of_me = t.x;
+        ov_me = t.y;
+      }
+      const int paddr = (sk * GW + (int)((rho_i >> (4 * w)) & 0xFu)) << 2;
+      const int x = __builtin_amdgcn_ds_permute(paddr, inv);  // rank space: inventory of the rank-w warehouse
+      const int incl = group_scan<GW>(x, w);
+      const int need = d - (incl - x);  // demand left after the cheaper ranks
+      int f = need > 0 ? (need < x ? need : x) : 0;  // min(inv, max(0, d - prefix)): one v_med3
+      int rem;
+      if (split) {  // max_splits: only the first max_wh contributing ranks ship
+        uint32_t m = fold_groups<GW>(__ballot(f > 0));
+        if (__builtin_popcount(m) > maxwh) {
+          uint32_t keep = 0u;
+          for (int k = 0; k < maxwh; k++) {
+            keep |= m & (0u - m);
+            m &= m - 1u;
+          }
+          m = keep;
+        }
+        f = ((m >> w) & 1u) ? f : 0;
+        rem = d - group_scan<GW>(f, w);
+      } else {
+        rem = d - incl > 0 ? d - incl : 0;
+      }
+      const int fw = __builtin_amdgcn_ds_bpermute(paddr, f);  // back to the warehouse's lane
+      inv -= fw;
+      qsr += fw;
+      dsum += d;
+      u += rem;  // (meaningful in the SKU's last rank lane: the order's unfulfilled demand)
+      cnt += (int)((fold_groups<GW>(__ballot(fw > 0)) >> w) & 1u);
+      lost_cnt += __ballot(w == GW - 1 && rem > 0) != 0 ? 1 : 0;
+    }
+    wave_sync();  // the window is rewritten next
+  }
+  if (cur >= 0) epilogue(cur);
+
+  // penalty (reward_calculator.py:134-137): (lost_sales * per-SKU cost or sku_weights * cost) summed
+  // over SKUs in order
+  Lw->dscr[lane] = pps ? lost * pen_me : (lost * skw_me) * pen_me;
+  wave_sync();
+  if (lv) {
+    s.inv[gi] = inv;
+    s.sc_sht[gi] = inv0 - inv;  // shipped this step = the inventory drop
+    s.sc_shh[gi] = home_done ? shh_h : 0;
+    if (home_done) s.inc[gi] = inc_h;  // (step_a zeroed it: a home region without orders leaves 0)
+    if (dbg) {
+      if (info.lost_sales) info.lost_sales[e * WK + w * K + sk] = lost;
+      if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] = inv0 - inv;
+    }
+    if (sk == 0) {
+      double pen = 0.0;
+#pragma unroll
+      for (int j = 0; j < K; j++) pen += Lw->dscr[j * GW + w];
+      s.sc_pen[w * E + e] = pen;
+      s.sc_out[w * E + e] = ofix + ovar;
+    }
+  }
+}
+
+size_t alloc_scan_lds_bytes(const EnvConst& c) {
+  const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : 8;
+  const size_t t = sc_tab_bytes(c.R, GW);
+  return (t <= SC_TAB_MAX ? t : 0) + SC_WAVES * sizeof(ScWaveLds);
+}
+bool alloc_scan_supported(int W, int K) { return W <= 8 && K <= 6; }
+
+template <int K>
+static void launch_scan_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
+  using KFn = void (*)(const DevEnv*, StepIO);
+  KFn f = c.W <= 2 ? (KFn)alloc_scan_kernel<K, 2> : c.W <= 4 ? (KFn)alloc_scan_kernel<K, 4> : (KFn)alloc_scan_kernel<K, 8>;
+  hipLaunchKernelGGL(f, dim3((unsigned)((c.E + SC_WAVES - 1) / SC_WAVES)), dim3(64 * SC_WAVES), alloc_scan_lds_bytes(c), st, d, io);
+}
+
+hipError_t launch_alloc_scan(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
+  if (!alloc_scan_supported(c.W, c.K)) return hipErrorInvalidValue;
+  switch (c.K) {
+    case 1: launch_scan_k<1>(c, d, io, st); break;
+    case 2: launch_scan_k<2>(c, d, io, st); break;
+    case 3: launch_scan_k<3>(c, d, io, st); break;
+    case 4: launch_scan_k<4>(c, d, io, st); break;
+    case 5: launch_scan_k<5>(c, d, io, st); break;
+    case 6: launch_scan_k<6>(c, d, io, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace msc

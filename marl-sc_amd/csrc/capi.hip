@@ -59,18 +59,82 @@ struct msc_env {
   // msc_env_set_timing: event pairs around demand / step launches (2 per launch)
   std::vector<hipEvent_t> tev_dem, tev_step;
   int t_cap = 0, n_tdem = 0, n_tstep = 0;
+  // Episode-ahead demand (EA; few envs per GPU). A Poisson episode's orders
+  // depend only on its seed (SeedSequence([root, counter]), seed_manager.py:100-120), not on
+  // actions, so whole future episodes are generated on `ea_stream` while earlier ones step: slot
+  // n % S holds episode n (counted from the snapshot taken when EA started, episode 0 = the one
+  // running then, which keeps the per-step path). At the end of episode n its slot is refilled
+  // with episode n + S. Any desynchronising event (masked reset, load_state, disabling) stops it;
+  // it restarts at the next common episode start.
+  bool ea_enabled = false;  // configured: Poisson demand, few envs (or MSC_EA=1), buffers allocated
+  bool ea_running = false;
+  int64_t ea_n = 0;         // episode (relative to the snapshot) the envs are in
+  int ea_cur = -1;          // slot of the current episode, -1: per-step demand
+  void* ea_mem = nullptr;
+  hipStream_t ea_stream = nullptr;
+  hipEvent_t ev_gen[MSC_EA_MAX_S] = {}, ev_cons[MSC_EA_MAX_S] = {}, ev_snap = nullptr;
+  std::vector<hipEvent_t> tev_ea;  // timing of EA launches (msc_env_set_timing)
+  int n_tea = 0;
 };
 
 static void timing_free(msc_env* env) {
   for (hipEvent_t e : env->tev_dem) (void)hipEventDestroy(e);
   for (hipEvent_t e : env->tev_step) (void)hipEventDestroy(e);
+  for (hipEvent_t e : env->tev_ea) (void)hipEventDestroy(e);
   env->tev_dem.clear();
   env->tev_step.clear();
-  env->t_cap = env->n_tdem = env->n_tstep = 0;
+  env->tev_ea.clear();
+  env->t_cap = env->n_tdem = env->n_tstep = env->n_tea = 0;
 }
 // record event `i` (0 = before, 1 = after) of launch n of `v` on `st`, if timing is on
 static hipError_t tmark(const msc_env* env, const std::vector<hipEvent_t>& v, int n, int i, hipStream_t st) {
   return n < env->t_cap ? hipEventRecord(v[2 * n + i], st) : hipSuccess;
+}
+
+// ---- episode-ahead demand (see msc_env) ----------------------------------------------------
+static hipError_t ea_launch(msc_env* env, int slot0, int nslots, int from_slot, int iters0) {
+  const bool tm = env->n_tea < env->t_cap;
+  if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea], env->ea_stream);
+  hipError_t e = launch_demand_ea(env->c, env->dev, EaLaunch{slot0, nslots, from_slot, iters0}, env->ea_stream);
+  if (e != hipSuccess) return e;
+  if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea++ + 1], env->ea_stream);
+  for (int k = 0; k < nslots; k++) {
+    e = hipEventRecord(env->ev_gen[(slot0 + k) % env->c.ea_S], env->ea_stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+// Snapshot at a common episode start (t_sync == 0, after the reset): the SeedManager counter of
+// the current episode -> slot 0's counter; episodes 1 .. S-1 are generated in one launch.
+static int ea_start(msc_env* env, hipStream_t st) {
+  const int S = env->c.ea_S;
+  HIP_TRY(hipEventRecord(env->ev_snap, env->ea_stream));  // EA work of an earlier run still reads ea_cnt
+  HIP_TRY(hipStreamWaitEvent(st, env->ev_snap, 0));
+  HIP_TRY(hipMemcpyAsync(env->s.ea_cnt, env->s.counter, sizeof(int32_t) * env->c.E, hipMemcpyDeviceToDevice, st));
+  HIP_TRY(hipEventRecord(env->ev_snap, st));
+  HIP_TRY(hipStreamWaitEvent(env->ea_stream, env->ev_snap, 0));
+  HIP_TRY(ea_launch(env, 1, S - 1, 0, 1));
+  env->ea_running = true;
+  env->ea_n = 0;
+  env->ea_cur = -1;
+  return 0;
+}
+// The demand stream of the current EA episode into s.rng[0] (what the per-step path and
+// read_state / save_state use), stream-ordered on st.
+static int ea_materialize(const msc_env* env, hipStream_t st) {
+  if (env->ea_running && env->ea_cur >= 0 && env->t_sync > 0)
+    HIP_TRY(launch_ea_materialize(env->c, env->dev, env->ea_cur, env->t_sync, st));
+  return 0;
+}
+static int ea_stop(msc_env* env, hipStream_t st, bool materialize) {
+  if (!env->ea_running) return 0;
+  if (materialize) {
+    const int rc = ea_materialize(env, st);
+    if (rc) return rc;
+  }
+  env->ea_running = false;
+  env->ea_cur = -1;
+  return 0;
 }
 
 extern "C" {
@@ -280,6 +344,28 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     }
     c.sort_shift = 0;
     while ((maxc >> c.sort_shift) >= SORT_BUCKETS) c.sort_shift++;
+    // few envs (BASELINE configs[1]: 4,096): the scan allocator (one env per wave, no
+    // data-dependent loop per order) when the shape fits it (<= 8 warehouses, <= 6 SKUs)
+    if (c.alloc_impl == 1 && alloc_scan_supported(W, K)) c.alloc_impl = 2;
+    if (const char* al = getenv("MSC_ALLOC_IMPL"))
+      if (strcmp(al, "scan") == 0) c.alloc_impl = alloc_scan_supported(W, K) ? 2 : 1;
+    // episode-ahead Poisson demand when the envs are too few to fill the chip with per-step demand
+    // chains (MSC_EA=0|1 forces it off / on)
+    c.ea_S = 0;
+    if (d->demand_type == MSC_DEMAND_POISSON) {
+      bool want = n_envs <= 8192;
+      if (const char* ea = getenv("MSC_EA")) want = atoi(ea) != 0;
+      int S = 8;
+      if (const char* es = getenv("MSC_EA_SLOTS")) S = atoi(es);
+      S = S < 2 ? 2 : (S > MSC_EA_MAX_S ? MSC_EA_MAX_S : S);
+      if (want) {
+        double lam_sum = 0.0;
+        for (int r = 0; r < R; r++) lam_sum += d->lambda_orders[r];
+        const double m = lam_sum * d->episode_length;
+        c.ea_S = S;
+        c.ea_cap = (int64_t)ceil(m + 12.0 * sqrt(m + 1.0) + 64.0);
+      }
+    }
   }
 
   TablePack tp;
@@ -320,6 +406,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     if (env->arena) (void)hipFree(env->arena);
     if (env->scratch) (void)hipFree(env->scratch);
     if (env->dev) (void)hipFree(env->dev);
+    if (env->ea_mem) (void)hipFree(env->ea_mem);
     delete env;
     return rc;
   };
@@ -423,6 +510,25 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       sb.n_orders = (int32_t*)(base + rec_bytes);
     }
   }
+  if (c.ea_S > 0) {  // episode-ahead buffers; without the memory EA stays off
+    const int S = c.ea_S, T = c.T;
+    const size_t rec = sizeof(uint4) * (size_t)nv * c.ea_cap * S * E;
+    const size_t offb = sizeof(int32_t) * (size_t)S * (T + 1) * E, posb = sizeof(uint32_t) * (size_t)S * T * E;
+    const size_t cntb = sizeof(int32_t) * (size_t)S * E;
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    if (hipMalloc(&env->ea_mem, al(rec) + al(offb) + al(posb) + al(cntb)) == hipSuccess) {
+      char* b = (char*)env->ea_mem;
+      s.ea_rec = s2.ea_rec = (uint4*)b;
+      s.ea_off = s2.ea_off = (int32_t*)(b + al(rec));
+      s.ea_pos = s2.ea_pos = (uint32_t*)(b + al(rec) + al(offb));
+      s.ea_cnt = s2.ea_cnt = (int32_t*)(b + al(rec) + al(offb) + al(posb));
+      env->ea_enabled = true;
+    } else {
+      (void)hipGetLastError();
+      env->ea_mem = nullptr;
+      c.ea_S = 0;
+    }
+  }
   // root seeds: explicit, or SeedSequence([base_seed, worker_index, env_index])
   std::vector<uint32_t> roots(E);
   std::vector<int32_t> minus1(E, -1);
@@ -467,6 +573,20 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     (void)hipEventRecord(env->ev_step[b], env->side);
   }
   (void)hipEventRecord(env->ev_reset, env->side);
+  if (env->ea_enabled) {
+    if (hipStreamCreateWithFlags(&env->ea_stream, hipStreamNonBlocking) != hipSuccess)
+      return fail(set_err(-2, "EA stream creation failed"));
+    for (int j = 0; j < MSC_EA_MAX_S; j++)
+      if (hipEventCreateWithFlags(&env->ev_gen[j], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&env->ev_cons[j], hipEventDisableTiming) != hipSuccess)
+        return fail(set_err(-2, "event creation failed"));
+    if (hipEventCreateWithFlags(&env->ev_snap, hipEventDisableTiming) != hipSuccess)
+      return fail(set_err(-2, "event creation failed"));
+    for (int j = 0; j < MSC_EA_MAX_S; j++) {
+      (void)hipEventRecord(env->ev_gen[j], env->ea_stream);
+      (void)hipEventRecord(env->ev_cons[j], env->ea_stream);
+    }
+  }
   *out = env;
   return 0;
 }
@@ -484,8 +604,15 @@ void msc_env_destroy(msc_env* env) {
     if (env->ev_step[b]) (void)hipEventDestroy(env->ev_step[b]);
   }
   if (env->ev_reset) (void)hipEventDestroy(env->ev_reset);
+  for (int j = 0; j < MSC_EA_MAX_S; j++) {
+    if (env->ev_gen[j]) (void)hipEventDestroy(env->ev_gen[j]);
+    if (env->ev_cons[j]) (void)hipEventDestroy(env->ev_cons[j]);
+  }
+  if (env->ev_snap) (void)hipEventDestroy(env->ev_snap);
+  if (env->ea_mem) (void)hipFree(env->ea_mem);
   timing_free(env);
   if (env->side) (void)hipStreamDestroy(env->side);
+  if (env->ea_stream) (void)hipStreamDestroy(env->ea_stream);
   delete env;
 }
 
@@ -506,6 +633,9 @@ int msc_env_reset(msc_env* env, const uint8_t* mask, const uint32_t* new_root_se
                   msc_stream_t stream) {
   if (!env) return set_err(-1, "null env");
   hipStream_t st = (hipStream_t)stream;
+  // episode-ahead demand stops (it restarts at the next common episode start); envs outside a
+  // mask keep their episode, so their demand stream is materialised first
+  if (const int rc = ea_stop(env, st, mask != nullptr)) return rc;
   // a reset re-seeds the demand streams: drop any demand generated ahead, order after the
   // side stream's last use of the state
   HIP_TRY(hipStreamWaitEvent(st, env->ev_dem[0], 0));
@@ -555,7 +685,17 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
   }
   const bool poisson = c.demand_type == MSC_DEMAND_POISSON;
   const int b = (int)(env->tau & 1);
-  if (poisson) {
+  // episode-ahead demand: start at a common episode start; an episode n >= 1 reads its slot
+  if (env->ea_enabled && env->pipeline && !env->ea_running && env->t_sync == 0)
+    if (const int rc = ea_start(env, st)) return rc;
+  if (env->ea_running && env->t_sync == 0) {
+    env->ea_cur = env->ea_n >= 1 ? (int)(env->ea_n % c.ea_S) : -1;
+    if (env->ea_cur >= 0) HIP_TRY(hipStreamWaitEvent(st, env->ev_gen[env->ea_cur], 0));
+  }
+  io.ea_slot = env->ea_running ? env->ea_cur : -1;
+  io.ea_t = env->t_sync;
+  const bool ea_step = io.ea_slot >= 0;
+  if (poisson && !ea_step) {
     if (env->ready[b]) {
       HIP_TRY(hipStreamWaitEvent(st, env->ev_dem[b], 0));
     } else {
@@ -571,7 +711,16 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
   HIP_TRY(hipEventRecord(env->ev_step[b], st));
   env->ready[b] = false;
   const bool boundary = env->t_sync < 0 || env->t_sync + 1 >= c.T;
-  if (env->pipeline && !boundary) {
+  if (env->ea_running && env->t_sync + 1 >= c.T) {
+    // episode ea_n ends with this step: its slot is refilled with episode ea_n + S once the step
+    // has read it
+    const int slot = (int)(env->ea_n % c.ea_S);
+    HIP_TRY(hipEventRecord(env->ev_cons[slot], st));
+    HIP_TRY(hipStreamWaitEvent(env->ea_stream, env->ev_cons[slot], 0));
+    HIP_TRY(ea_launch(env, slot, 1, slot, c.ea_S));
+    env->ea_n++;
+  }
+  if (env->pipeline && !boundary && !ea_step) {
     // demand of step tau+1 into the other buffer, concurrently with this step kernel; that buffer
     // was last read by step tau-1, and the demand stream was last advanced by demand(tau)
     const int nb = b ^ 1;
@@ -592,6 +741,12 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
 int msc_env_set_pipelining(msc_env* env, int32_t enabled) {
   if (!env) return set_err(-1, "null env");
   env->pipeline = enabled != 0 && env->c.demand_type == MSC_DEMAND_POISSON;
+  if (!env->pipeline && env->ea_running) {  // back to per-step demand from the current step on
+    HIP_TRY(hipSetDevice(env->device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (const int rc = ea_stop(env, nullptr, true)) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+  }
   return 0;
 }
 
@@ -613,11 +768,13 @@ int msc_env_set_timing(msc_env* env, int32_t max_steps) {
   HIP_TRY(hipDeviceSynchronize());
   timing_free(env);
   for (int i = 0; i < 2 * max_steps; i++) {
-    hipEvent_t a, b;
+    hipEvent_t a, b, x;
     HIP_TRY(hipEventCreate(&a));
     HIP_TRY(hipEventCreate(&b));
+    HIP_TRY(hipEventCreate(&x));
     env->tev_dem.push_back(a);
     env->tev_step.push_back(b);
+    env->tev_ea.push_back(x);
   }
   env->t_cap = max_steps;
   return 0;
@@ -646,9 +803,28 @@ int msc_env_read_timing(msc_env* env, double* demand_ms, double* step_ms, int64_
   return 0;
 }
 
+int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* slots, int32_t* active) {
+  if (!env) return set_err(-1, "null env");
+  const int n = env->n_tea < env->t_cap ? env->n_tea : env->t_cap;
+  double sum = 0.0;
+  for (int i = 0; i < n; i++) {
+    HIP_TRY(hipEventSynchronize(env->tev_ea[2 * i + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, env->tev_ea[2 * i], env->tev_ea[2 * i + 1]));
+    sum += ms;
+  }
+  if (ea_ms) *ea_ms = n ? sum / n : 0.0;
+  if (n_ea) *n_ea = n;
+  if (slots) *slots = env->c.ea_S;
+  if (active) *active = env->ea_running && env->ea_cur >= 0 ? 1 : 0;
+  return 0;
+}
+
 int msc_env_generate_demand(msc_env* env, msc_stream_t stream) {
   if (!env) return set_err(-1, "null env");
   if (env->c.demand_type != MSC_DEMAND_POISSON) return 0;
+  // the next step reads an episode-ahead slot: nothing to generate
+  if (env->ea_running && (env->t_sync == 0 ? env->ea_n >= 1 : env->ea_cur >= 0)) return 0;
   const int b = (int)(env->tau & 1);
   if (env->ready[b]) return 0;  // already generated ahead
   hipStream_t st = (hipStream_t)stream;
@@ -671,6 +847,10 @@ int msc_env_read_state(const msc_env* env, int32_t* inv, int32_t* ts, int32_t* e
   if (!env) return set_err(-1, "null env");
   const int64_t E = env->c.E, WK = (int64_t)env->c.W * env->c.K;
   HIP_TRY(hipDeviceSynchronize());
+  if (rng && env->ea_running && env->ea_cur >= 0 && env->t_sync > 0) {
+    if (const int rc = ea_materialize(env, nullptr)) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+  }
   if (inv) {
     std::vector<int32_t> soa(WK * E);
     HIP_TRY(hipMemcpy(soa.data(), env->s.inv, sizeof(int32_t) * WK * E, hipMemcpyDeviceToHost));
@@ -714,6 +894,10 @@ int64_t msc_env_state_bytes(const msc_env* env) {
 int msc_env_save_state(const msc_env* env, void* buf) {
   if (!env || !buf) return set_err(-1, "null argument");
   HIP_TRY(hipDeviceSynchronize());
+  if (env->ea_running && env->ea_cur >= 0 && env->t_sync > 0) {  // the blob carries the demand stream
+    if (const int rc = ea_materialize(env, nullptr)) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+  }
   const int b = (int)(env->tau & 1);
   StateHeader h{STATE_MAGIC, env->ready[b] ? 1u : 0u, env->t_sync, 0};
   memcpy(buf, &h, sizeof h);
@@ -731,6 +915,7 @@ int msc_env_load_state(msc_env* env, const void* buf) {
   memcpy(&h, buf, sizeof h);
   if (h.magic != STATE_MAGIC) return set_err(-1, "not a libmarlsc state blob");
   HIP_TRY(hipDeviceSynchronize());
+  if (const int rc = ea_stop(env, nullptr, false)) return rc;  // restarts at the next episode start
   const char* p = (const char*)buf + sizeof h;
   HIP_TRY(hipMemcpy(env->arena, p, env->arena_bytes, hipMemcpyHostToDevice));
   const int b = (int)(env->tau & 1);
@@ -796,10 +981,26 @@ int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_
   if (!x || !w1p || !b1 || !w2p || !b2 || !w3p || !b3 || !out) return set_err(-1, "null argument");
   if (n_rows < 0 || in_dim < 1 || in_dim > 1024 || out_dim < 1 || out_dim > 32)
     return set_err(-1, "bad shape (n_rows %lld, in_dim %d, out_dim %d)", (long long)n_rows, in_dim, out_dim);
-  if (!(hidden1 == hidden2 && (hidden1 == 64 || hidden1 == 128 || hidden1 == 256)))
-    return set_err(-1, "hidden sizes %d, %d: the fused MLP supports [64, 64], [128, 128] and [256, 256]", hidden1, hidden2);
+  auto hs = [](int h) { return h == 64 || h == 128 || h == 256 || h == 512; };
+  if (!(hs(hidden1) && hs(hidden2)))
+    return set_err(-1, "hidden sizes %d, %d: the fused MLP supports [H1, H2] with H1, H2 in {64, 128, 256, 512}", hidden1, hidden2);
   HIP_TRY(launch_mlp3_relu(x, n_rows, in_dim, hidden1, hidden2, out_dim, w1p, b1, w2p, b2, w3p, b3, out, pre1,
                            pre1 ? pre1_group : 1, (hipStream_t)stream));
+  return 0;
+}
+
+int msc_mlp2_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden, int32_t out_dim,
+                          const float* w1p, const float* b1, const float* w3p, const float* b3, float* out,
+                          const float* pre1, int32_t pre1_group, msc_stream_t stream) {
+  if (pre1 && pre1_group < 1) return set_err(-1, "pre1_group %d must be >= 1", pre1_group);
+  if (((uintptr_t)b1 | (uintptr_t)pre1 | (uintptr_t)w1p | (uintptr_t)w3p) & 15)
+    return set_err(-1, "b1, pre1 and the packed weights must be 16-byte aligned");
+  if (!x || !w1p || !b1 || !w3p || !b3 || !out) return set_err(-1, "null argument");
+  if (n_rows < 0 || in_dim < 1 || in_dim > 1024 || out_dim < 1 || out_dim > 32)
+    return set_err(-1, "bad shape (n_rows %lld, in_dim %d, out_dim %d)", (long long)n_rows, in_dim, out_dim);
+  if (!mlp2_supported(hidden)) return set_err(-1, "hidden size %d: the fused MLP supports multiples of 32 up to 1024", hidden);
+  HIP_TRY(launch_mlp2_relu(x, n_rows, in_dim, hidden, out_dim, w1p, b1, w3p, b3, out, pre1, pre1 ? pre1_group : 1,
+                           (hipStream_t)stream));
   return 0;
 }
 
@@ -821,6 +1022,9 @@ int msc_env_set_episode_counters(msc_env* env, const int32_t* counters_host) {
   for (int64_t i = 0; i < E; i++)
     if (counters_host[i] < 0) return set_err(-1, "episode counter %d of env %lld is negative", counters_host[i], (long long)i);
   HIP_TRY(hipSetDevice(env->device));
+  HIP_TRY(hipDeviceSynchronize());
+  // episodes generated ahead assumed the old counters: stop (restarts at the next episode start)
+  if (const int rc = ea_stop(env, nullptr, true)) return rc;
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(env->s.counter, counters_host, sizeof(int32_t) * E, hipMemcpyHostToDevice));
   return 0;

@@ -23,6 +23,7 @@ namespace msc {
 
 constexpr int BS = 64;          // threads per block of the env kernels (one wave: one env per lane)
 constexpr int MAX_RING = 64;    // pending-order ring slots (max actual lead time + 1)
+#define MSC_EA_MAX_S 16   // episode-ahead demand: max episode slots per env
 
 struct EnvConst {
   int32_t W, K, R, T, Lmax, RING, F, L, order_cap;
@@ -41,8 +42,10 @@ struct EnvConst {
   int32_t chain_prio;   // step_a / step_c waves at s_setprio 3 (msc_env_set_chain_priority)
   int32_t alloc_sort;   // step_b_kernel visits envs in descending order of this step's order count (perm)
   int32_t sort_shift;   // order count >> sort_shift = bucket (< SORT_BUCKETS)
+  int32_t ea_S;         // episode-ahead demand: episode slots per env (0: off)
   uint32_t flags;
   int64_t E;
+  int64_t ea_cap;       // episode-ahead demand: order records per (slot, env) episode
   double scale, alpha, hold_scalar, pen_scalar;
   double uni_thr_o, uni_thr_m, uni_thr_q;  // demand_uni: exp(-lambda_orders), p_skip, exp(-lambda_quantity)
   const MSC_G double* act_param;   // [K]
@@ -96,6 +99,26 @@ struct EnvState {
   MSC_G double* sc_out;
   MSC_G double* sc_inb;
   MSC_G uint32_t* err;       // [1] device error bits
+  // episode-ahead demand (EA): the Poisson orders of whole future episodes,
+  // generated on a side stream while earlier episodes step. Slot j of env e holds one episode:
+  uint4* ea_rec;             // [S][E][ea_cap][NV] order records, each env's episode contiguous
+  MSC_G int32_t* ea_off;     // [S][T + 1][E] first record of step t (off[T] = the episode's count)
+  MSC_G uint32_t* ea_pos;    // [S][T][E]     demand-stream position (draws) after step t
+  MSC_G int32_t* ea_cnt;     // [S][E]        SeedManager._episode_counter after the slot episode's reset
+};
+
+// one launch of the episode-ahead demand generator: lanes (k, e) for k < nslots generate the
+// episode of slot (slot0 + k) % S; its SeedManager counter follows from the counter stored for
+// from_slot by iters0 + k more resets (reset_env's eval cycling included)
+struct EaLaunch {
+  int32_t slot0, nslots, from_slot, iters0;
+};
+
+// where an env's orders of this step are: record n, word v at base + n * nstep + v * vstep (uint4)
+struct OrderSrc {
+  const uint4* src;
+  int64_t base, nstep, vstep;
+  int n;
 };
 
 struct StepIO {
@@ -107,7 +130,46 @@ struct StepIO {
   MSC_G float* final_obs;      // [E][W][L] or null
   msc_step_info info;    // device pointers or nulls
   int32_t has_info;
+  int32_t ea_slot;       // >= 0: this step's orders come from episode-ahead slot ea_slot, step ea_t
+  int32_t ea_t;
 };
+
+// The orders of env e for this step (every allocation kernel reads them through this): the Poisson
+// sampler's per-step buffer [order][NV][E], an episode-ahead slot, or the empirical trace row.
+template <int NV>
+__device__ __forceinline__ OrderSrc order_src(const EnvConst& c, const EnvState& s, const StepIO& io, int64_t e) {
+  OrderSrc o;
+  const int64_t E = c.E;
+  if (c.demand_type == MSC_DEMAND_EMPIRICAL) {
+    o.src = c.tr_rec;
+    o.nstep = NV;
+    o.vstep = 1;
+    o.base = 0;
+    o.n = 0;
+    if (s.emp_start[e] >= 0) {
+      const int64_t row = s.emp_start[e] + (s.t[e] % c.T);
+      const int64_t off = c.tr_off[row];
+      o.n = (int)(c.tr_off[row + 1] - off);
+      o.base = off * NV;
+    }
+  } else if (io.ea_slot >= 0) {
+    const int64_t le = (int64_t)io.ea_slot * E + e;
+    const MSC_G int32_t* off = s.ea_off + ((int64_t)io.ea_slot * (c.T + 1) + io.ea_t) * E + e;
+    const int o0 = off[0];
+    o.src = s.ea_rec;
+    o.n = off[E] - o0;
+    o.base = (le * c.ea_cap + o0) * NV;
+    o.nstep = NV;
+    o.vstep = 1;
+  } else {
+    o.src = s.orders;
+    o.n = s.n_orders[e];
+    o.base = e;
+    o.nstep = (int64_t)NV * E;
+    o.vstep = E;
+  }
+  return o;
+}
 
 constexpr uint32_t ERR_ORDER_OVERFLOW = 1u;
 
@@ -123,6 +185,11 @@ hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask,
                         int32_t flags, float* obs, hipStream_t st);
 hipError_t launch_step(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen_demand, hipStream_t st);
 hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st);
+hipError_t launch_demand_ea(const EnvConst& c, const DevEnv* d, const EaLaunch& ea, hipStream_t st);
+hipError_t launch_ea_materialize(const EnvConst& c, const DevEnv* d, int slot, int t_done, hipStream_t st);
+// alloc_scan.hip
+hipError_t launch_alloc_scan(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
+bool alloc_scan_supported(int W, int K);
 constexpr int SORT_BUCKETS = 1024;
 // alloc_kernels.hip
 hipError_t launch_alloc_lane(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
@@ -138,6 +205,9 @@ int mlp3_valu_outputs(int KO);
 hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, int KO, const float* w1p, const float* b1,
                             const float* w2p, const float* b2, const float* w3p, const float* b3, float* out,
                             const float* pre1, int grp, hipStream_t st);
+hipError_t launch_mlp2_relu(const float* x, int64_t n, int L, int H1, int KO, const float* w1p, const float* b1,
+                            const float* w3p, const float* b3, float* out, const float* pre1, int grp, hipStream_t st);
+bool mlp2_supported(int H1);
 hipError_t launch_gauss_sample(const float* mean, const float* log_std, int32_t ls_rows, float floor_, const float* eps,
                                int64_t N, int32_t K, float* act, float* logp, float* clipped, hipStream_t st);
 

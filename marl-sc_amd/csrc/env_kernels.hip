@@ -622,6 +622,22 @@ __device__ __forceinline__ int unit_quota(int tgt, int rdp) {
   return q < cap ? q : cap;
 }
 
+// EA: the root seed of the episode a lane generates (reset_env's counter rule applied iters0 + k
+// times from the counter stored for from_slot); the counter after that reset goes to cnt_out
+__device__ __forceinline__ uint32_t ea_root(const EnvConst& c, const EnvState& s, const EaLaunch& ea, int64_t e,
+                                            int k, int& cnt_out) {
+  int cnt = s.ea_cnt[(int64_t)ea.from_slot * c.E + e];
+  const int iters = ea.iters0 + k;
+  int wv = 0;
+  for (int i = 0; i < iters; i++) {
+    wv = (c.num_eval > 0 && cnt >= c.num_eval) ? 0 : cnt;
+    cnt = wv + 1;
+  }
+  cnt_out = cnt;
+  const uint32_t w2[2] = {s.orig_root[e], (uint32_t)wv};
+  return ss_u32(w2, 2);
+}
+
 __host__ __device__ constexpr size_t unit_lds_fixed() {
   return (size_t)BS * USLOTS * sizeof(double) + (size_t)2 * BS * sizeof(int32_t);
 }
@@ -638,9 +654,13 @@ __host__ __device__ constexpr size_t unit_lds_fixed() {
 // UNI: every region has the same lambda_orders, probability_skus and lambda_quantity (scalar
 // sampler parameters, demand_sampler.py:99-102, or equal per-region arrays): the three thresholds
 // live in scalar registers and the settle step needs no table reads or region-indexed addressing.
-template <int K, int G, bool LDS_TAB, bool UNI>
+// EA (episode-ahead demand): lane = (slot, env) of a future episode; the
+// parser runs all T steps of the episode back to back (at the end of a step's last region it starts
+// region 0 of the next step) and writes the orders env-contiguously into the slot, with the record
+// offset and stream position at every step boundary.
+template <int K, int G, bool LDS_TAB, bool UNI, bool EA>
 __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MSC_DEM_WPE))) void demand_unit_kernel(
-    const DevEnv* __restrict__ dp) {
+    const DevEnv* __restrict__ dp, EaLaunch ea) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int R = c.R;
@@ -669,9 +689,28 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
                 : c.parser_rot == 3 ? (int)(blockIdx.x >> 3) : 0;
   const int wave = ((int)(threadIdx.x / BS) + rot) % (1 + G), lane = threadIdx.x % BS;  // role 0 parses
   const int64_t E = c.E;
-  const int64_t e = (int64_t)blockIdx.x * c.epw_dem + lane;
-  const bool valid = lane < c.epw_dem && e < E;
+  const int64_t vlane = (int64_t)blockIdx.x * c.epw_dem + lane;
+  int64_t e = vlane;
+  int slot = 0, ea_k = 0;
+  bool valid = lane < c.epw_dem && vlane < E;
+  if constexpr (EA) {
+    valid = lane < c.epw_dem && vlane < (int64_t)ea.nslots * E;
+    ea_k = valid ? (int)(vlane / E) : 0;
+    e = valid ? vlane - (int64_t)ea_k * E : 0;
+    slot = (ea.slot0 + ea_k) % c.ea_S;
+  }
   double* myring = ring + lane;
+  int ea_cnt_new = 0;
+  auto start_rng = [&]() -> Pcg64 {
+    if constexpr (EA) {
+      uint32_t root = ea_root(c, s, ea, e, ea_k, ea_cnt_new);
+      Pcg64 r;
+      pcg_seed_child(r, root, 2);  // 'demand_sampler' child of the episode's root (seed_manager.py:100-120)
+      return r;
+    } else {
+      return load_rng(s, 0, e, E);
+    }
+  };
 
   if (wave > 0) {
     // ---------------- generator g: stream positions g, g + G, g + 2G, ...
@@ -679,7 +718,7 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     const int g = wave - 1;
     uint64_t th = 0, tl = 0, ih = 0, il = 1;
     if (valid) {
-      Pcg64 rg = load_rng(s, 0, e, E);
+      Pcg64 rg = start_rng();
       for (int j = 0; j <= g; j++) pcg_step(rg);
       th = rg.s_hi;
       tl = rg.s_lo;
@@ -729,21 +768,35 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   __builtin_amdgcn_s_setprio(MSC_PARSER_PRIO);
   Pcg64 r0{};
   if (valid) {
-    r0 = load_rng(s, 0, e, E);
-    store_rng_pre(s, e, E, r0);
+    r0 = start_rng();
+    if constexpr (!EA) store_rng_pre(s, e, E, r0);
   }
   rdv[lane] = 0;
   static_assert(K <= UD, "a mask unit completes in one round");
   int st = valid ? PS_ORD : PS_DONE, r = 0, x = 0, left = 0, sq = 0, n = 0, rd = 0;
+  int tstep = 0;  // EA: step of the episode being parsed
   unsigned mask = 0;
   int mf = 0, live = valid ? 1 : 0, pend = 0;
-  const int cap = c.order_cap;
+  const int cap = EA ? (int)c.ea_cap : c.order_cap;
   // the current order's record: written as {region, 0, ..., 0} when the order starts, then each
   // SKU quantity is stored into its 16-bit field as its unit ends (same-lane stores to one
   // address stay in program order)
-  const int64_t rstride = (int64_t)NV * E * 16;  // bytes between consecutive records of a lane
-  MSC_GLOBAL char* recp = reinterpret_cast<MSC_GLOBAL char*>(gp(s.orders + e)) - rstride;
+  const int64_t vstride = EA ? 16 : E * 16;       // bytes between the uint4 words of a record
+  const int64_t rstride = (int64_t)NV * vstride;  // bytes between consecutive records of a lane
+  MSC_GLOBAL char* recp = reinterpret_cast<MSC_GLOBAL char*>(
+      gp(EA ? s.ea_rec + ((int64_t)slot * E + e) * c.ea_cap * NV : s.orders + e)) - rstride;
+  // EA step boundaries: record offset / stream position after each step of the episode
+  decltype(s.ea_off) ea_offp = EA ? s.ea_off + (int64_t)slot * (c.T + 1) * E + e : nullptr;
+  decltype(s.ea_pos) ea_posp = EA ? s.ea_pos + (int64_t)slot * c.T * E + e : nullptr;
+  const int T_s = __builtin_amdgcn_readfirstlane(c.T);
   __syncthreads();
+  if constexpr (EA) {
+    // (after the barrier: every wave of the block has read the slot's previous counter)
+    if (valid) {
+      s.ea_cnt[(int64_t)slot * E + e] = ea_cnt_new;
+      ea_offp[0] = 0;
+    }
+  }
   // p_skip[r] and exp(-lambda_o[r + 1]) of the current region in registers (reloaded when a
   // region starts, long before their first use); exp(-lambda_q[r, sku]) is read from the LDS
   // table when a quantity unit opens, while the round's ring reads are in flight
@@ -761,7 +814,7 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     const int is_q = st == PS_QTY ? 1 : 0, is_o = st == PS_ORD ? 1 : 0;
     if (is_q & (n <= cap_s ? 1 : 0)) {
       const int h = 1 + sq;  // 16-bit field of the record (field 0 = region)
-      MSC_GLOBAL char* fp = NV == 1 ? recp + h * 2 : recp + (int64_t)(h >> 3) * E * 16 + (h & 7) * 2;
+      MSC_GLOBAL char* fp = NV == 1 ? recp + h * 2 : recp + (int64_t)(h >> 3) * vstride + (h & 7) * 2;
       *reinterpret_cast<MSC_GLOBAL uint16_t*>(fp) = (uint16_t)(x > 1 ? x : 1);  // max(1, Poisson(lambda_q))
     }
     const unsigned m2 = is_q ? (mask & (mask - 1u)) : mask;  // a mask unit left its bits in mask
@@ -770,7 +823,16 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     const int new_order = (has_q ^ 1) & (left2 > 0 ? 1 : 0);
     const int new_region = (has_q | new_order) ^ 1;
     sq = __builtin_ctz(m2 | (1u << K));
-    st = has_q ? PS_QTY : new_order ? PS_MASK : (r + new_region < R_s ? PS_ORD : PS_DONE);
+    int wrap = 0;  // EA: the step's last region ended and another step of the episode follows
+    if constexpr (EA) {
+      if (new_region & (r + 1 == R_s ? 1 : 0)) {
+        ea_offp[(int64_t)(tstep + 1) * E] = n;
+        ea_posp[(int64_t)tstep * E] = (uint32_t)rd;
+        wrap = tstep + 1 < T_s ? 1 : 0;
+        tstep += wrap;
+      }
+    }
+    st = has_q ? PS_QTY : new_order ? PS_MASK : ((r + new_region < R_s) | wrap ? PS_ORD : PS_DONE);
     // three-way threshold choice as a bit select (as a ?: chain the optimizer turns it into a lookup
     // table in scratch memory, which then keeps the whole parser state in scratch)
     {
@@ -788,9 +850,9 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     if (new_order & (n <= cap_s ? 1 : 0)) {
 #pragma unroll
       for (int j = 0; j < NV; j++)
-        *reinterpret_cast<MSC_GLOBAL v4u*>(recp + (int64_t)j * E * 16) = v4u{j == 0 ? (unsigned)r : 0u, 0u, 0u, 0u};
+        *reinterpret_cast<MSC_GLOBAL v4u*>(recp + (int64_t)j * vstride) = v4u{j == 0 ? (unsigned)r : 0u, 0u, 0u, 0u};
     }
-    r += new_region;
+    r = wrap ? 0 : r + new_region;
     prod = 1.0;
     x = 0;
     mf = st == PS_MASK ? 1 : 0;
@@ -802,19 +864,28 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     const int is_q = st == PS_QTY ? 1 : 0, is_o = st == PS_ORD ? 1 : 0;
     if (is_q & (n <= cap ? 1 : 0)) {
       const int h = 1 + sq;  // 16-bit field of the record (field 0 = region)
-      *reinterpret_cast<MSC_GLOBAL uint16_t*>(recp + (int64_t)(h >> 3) * E * 16 + (h & 7) * 2) =
+      *reinterpret_cast<MSC_GLOBAL uint16_t*>(recp + (int64_t)(h >> 3) * vstride + (h & 7) * 2) =
           (uint16_t)(x > 1 ? x : 1);  // max(1, Poisson(lambda_q))
     }
     const unsigned m2 = is_q ? (mask & (mask - 1u)) : mask;
     const int has_q = (is_o ^ 1) & (m2 != 0u ? 1 : 0);
     const int left2 = (is_o ? x : left) - ((is_o | has_q) ^ 1);  // an order completed
     const int new_order = (has_q ^ 1) & (left2 > 0 ? 1 : 0);
-    const int new_region = (has_q | new_order) ^ 1 ? (r + 1 < R ? 1 : 0) : 0;
+    int new_region = (has_q | new_order) ^ 1 ? (r + 1 < R ? 1 : 0) : 0;
     int nsq = __builtin_ctz(m2 | (1u << K));
     nsq = nsq < K ? nsq : K - 1;
     const double q_thr = Tq[r * K + nsq];
-    st = has_q ? PS_QTY : new_order ? PS_MASK : new_region ? PS_ORD : PS_DONE;
-    thr = has_q ? q_thr : new_order ? tk : to_next;
+    int wrap = 0;  // EA: the step's last region ended and another step of the episode follows
+    if constexpr (EA) {
+      if (((has_q | new_order) ^ 1) & (r + 1 == R ? 1 : 0)) {
+        ea_offp[(int64_t)(tstep + 1) * E] = n;
+        ea_posp[(int64_t)tstep * E] = (uint32_t)rd;
+        wrap = tstep + 1 < T_s ? 1 : 0;
+        tstep += wrap;
+      }
+    }
+    st = has_q ? PS_QTY : new_order ? PS_MASK : (new_region | wrap) ? PS_ORD : PS_DONE;
+    thr = has_q ? q_thr : new_order ? tk : wrap ? To[0] : to_next;
     sq = nsq;
     mask = new_order ? 0u : m2;
     left = left2;
@@ -823,9 +894,9 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     if (new_order & (n <= cap ? 1 : 0)) {
 #pragma unroll
       for (int j = 0; j < NV; j++)
-        *reinterpret_cast<MSC_GLOBAL v4u*>(recp + (int64_t)j * E * 16) = v4u{j == 0 ? (unsigned)r : 0u, 0u, 0u, 0u};
+        *reinterpret_cast<MSC_GLOBAL v4u*>(recp + (int64_t)j * vstride) = v4u{j == 0 ? (unsigned)r : 0u, 0u, 0u, 0u};
     }
-    r += new_region;
+    r = wrap ? 0 : r + new_region;
     tk = Tk[r];
     to_next = To[r + 1 < R ? r + 1 : r];
     prod = 1.0;
@@ -899,6 +970,10 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   PROF_FLUSH(5, n_chunk);
   PROF_FLUSH(6, 1ull);
   if (!valid) return;
+  if constexpr (EA) {
+    if (n > cap) atomicOr(s.err, ERR_ORDER_OVERFLOW);
+    return;
+  }
   pcg_advance(r0, (uint64_t)rd);
   store_rng(s, 0, e, E, r0);
   if (n > cap) {
@@ -906,6 +981,20 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     n = cap;
   }
   s.n_orders[e] = n;
+}
+
+// The demand stream of env e as of `t_done` steps into the episode held by EA slot `slot`
+// (read_state / save_state / leaving EA mode): the 'demand_sampler' child of the episode's root
+// (s.root, written by the reset that started it) advanced by the draws of those steps.
+__global__ void ea_materialize_kernel(const DevEnv* __restrict__ dp, int32_t slot, int32_t t_done) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= c.E || t_done < 1) return;
+  Pcg64 r;
+  pcg_seed_child(r, s.root[e], 2);
+  pcg_advance(r, s.ea_pos[((int64_t)slot * c.T + (t_done - 1)) * c.E + e]);
+  store_rng(s, 0, e, c.E, r);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1100,20 +1189,15 @@ __device__ __forceinline__ double group_np_sum(double v, int n) {
 #endif
 
 // This step's order count of env e (what step_b_kernel iterates over).
-__device__ __forceinline__ int step_order_count(const EnvConst& c, const EnvState& s, int64_t e) {
-  if (c.demand_type == MSC_DEMAND_EMPIRICAL) {
-    if (s.emp_start[e] < 0) return 0;
-    const int64_t row = s.emp_start[e] + (s.t[e] % c.T);
-    return (int)(c.tr_off[row + 1] - c.tr_off[row]);
-  }
-  return s.n_orders[e];
+__device__ __forceinline__ int step_order_count(const EnvConst& c, const EnvState& s, const StepIO& io, int64_t e) {
+  return order_src<1>(c, s, io, e).n;
 }
 
 // Allocation visiting order: envs by descending order count of this step (counting sort over
 // SORT_BUCKETS buckets of count >> sort_shift; the order within a bucket is arbitrary, as is any
 // permutation: every env's allocation is independent of where it runs). One block; ~10 us at
 // 8,192 envs. Busiest envs first also starts the longest waves first.
-__global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restrict__ dp) {
+__global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int64_t E = c.E;
@@ -1121,7 +1205,7 @@ __global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restri
   __shared__ int wsum[1024 / 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   auto key = [&](int64_t e) {
-    const int b = step_order_count(c, s, e) >> c.sort_shift;
+    const int b = step_order_count(c, s, io, e) >> c.sort_shift;
     return SORT_BUCKETS - 1 - (b < SORT_BUCKETS ? b : SORT_BUCKETS - 1);
   };
   for (int i = tid; i < SORT_BUCKETS; i += blockDim.x) hist[i] = 0;
@@ -1191,25 +1275,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
     qsr[sk] = 0;
   }
   double pen = 0.0, out = 0.0, cof = 0.0, cov = 0.0;
-  int n_orders = 0;
   // record (n, v) of this lane's env at base + n * nstep + v * vstep (uint4 units)
-  int64_t base = 0, nstep, vstep;
-  if (c.demand_type == MSC_DEMAND_EMPIRICAL) {
-    if (ev) {
-      const int64_t row = s.emp_start[e] + (s.t[e] % c.T);
-      const int64_t off = c.tr_off[row];
-      n_orders = (int)(c.tr_off[row + 1] - off);
-      base = off * NVR;
-    }
-    nstep = NVR;
-    vstep = 1;
-  } else {
-    n_orders = ev ? s.n_orders[e] : 0;
-    base = ev ? e : 0;
-    nstep = (int64_t)NVR * E;
-    vstep = E;
-  }
-  const MSC_GLOBAL uint4* src = gp(c.demand_type == MSC_DEMAND_EMPIRICAL ? c.tr_rec : s.orders);
+  const OrderSrc osrc = order_src<NVR>(c, s, io, ev ? e : 0);
+  const int n_orders = ev ? osrc.n : 0;
+  const int64_t base = ev ? osrc.base : 0, nstep = osrc.nstep, vstep = osrc.vstep;
+  const MSC_GLOBAL uint4* src = gp(osrc.src);
   if (dbg && ev && w == 0 && info.n_orders) info.n_orders[e] = n_orders;
   // loader role: lane l fetches records of env l % EPW of this wave (whose group leader is lane
   // (l % EPW) * GW); window slot q = j * 64 + l holds (order q / (EPW NVR), v, env q % EPW)
@@ -1643,32 +1713,52 @@ size_t demand_lds_bytes(const EnvConst& c) {
 }
 
 template <int K, int G>
-static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t st) {
+static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea) {
   using DFn = void (*)(const DevEnv*);
+  using UFn = void (*)(const DevEnv*, EaLaunch);
   const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
   const bool t = park_lds_tables(c);
-  DFn fn;
-  if (c.demand_impl == 5)  // 4-draw parking parser (A/B: MSC_DEMAND_IMPL=park4)
-    fn = t ? (DFn)demand_park4_kernel<K, G, true> : (DFn)demand_park4_kernel<K, G, false>;
-  else if (c.demand_uni)
-    fn = (DFn)demand_unit_kernel<K, G, false, true>;
-  else
-    fn = t ? (DFn)demand_unit_kernel<K, G, true, false> : (DFn)demand_unit_kernel<K, G, false, false>;
-  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), park_fixed(c) + (t && !c.demand_uni ? tab : 0), st, d);
+  const size_t lds = park_fixed(c) + (t && !c.demand_uni ? tab : 0);
+  if (ea) {  // episode-ahead generation over nslots x E lanes
+    const UFn fn = c.demand_uni ? (UFn)demand_unit_kernel<K, G, false, true, true>
+                                : (t ? (UFn)demand_unit_kernel<K, G, true, false, true> : (UFn)demand_unit_kernel<K, G, false, false, true>);
+    const size_t lds_u = unit_lds_fixed() + (t && !c.demand_uni ? tab : 0);
+    hipLaunchKernelGGL(fn, grid_for((int64_t)ea->nslots * c.E, c.epw_dem), dim3(BS * (1 + G)), lds_u, st, d, *ea);
+    return;
+  }
+  if (c.demand_impl == 5) {  // 4-draw parking parser (A/B: MSC_DEMAND_IMPL=park4)
+    const DFn fn = t ? (DFn)demand_park4_kernel<K, G, true> : (DFn)demand_park4_kernel<K, G, false>;
+    hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), lds, st, d);
+    return;
+  }
+  const UFn fn = c.demand_uni ? (UFn)demand_unit_kernel<K, G, false, true, false>
+                              : (t ? (UFn)demand_unit_kernel<K, G, true, false, false> : (UFn)demand_unit_kernel<K, G, false, false, false>);
+  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), lds, st, d, EaLaunch{0, 0, 0, 0});
 }
 
 template <int K>
-static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st) {
+static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea = nullptr) {
   if (c.demand_gen == 1)
-    launch_split_demand<K, 1>(c, d, st);
+    launch_split_demand<K, 1>(c, d, st, ea);
   else if (c.demand_gen == 2)
-    launch_split_demand<K, 2>(c, d, st);
+    launch_split_demand<K, 2>(c, d, st, ea);
   else
-    launch_split_demand<K, 3>(c, d, st);
+    launch_split_demand<K, 3>(c, d, st, ea);
 }
 
 hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st) {
   MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st));
+  return hipGetLastError();
+}
+
+hipError_t launch_demand_ea(const EnvConst& c, const DevEnv* d, const EaLaunch& ea, hipStream_t st) {
+  if (ea.nslots < 1) return hipSuccess;
+  MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st, &ea));
+  return hipGetLastError();
+}
+
+hipError_t launch_ea_materialize(const EnvConst& c, const DevEnv* d, int slot, int t_done, hipStream_t st) {
+  hipLaunchKernelGGL(ea_materialize_kernel, grid_for(c.E, 256), dim3(256), 0, st, d, slot, t_done);
   return hipGetLastError();
 }
 
@@ -1691,9 +1781,13 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
   const size_t lds_a = c.lead_type == MSC_LEAD_STOCHASTIC ? (size_t)c.W * K * BS * sizeof(int32_t) : 0;
   hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * c.W), lds_a, st, d, io);
   if (c.alloc_impl == 0) {
-    (void)launch_alloc_lane(c, d, io, st);
+    const hipError_t ea = launch_alloc_lane(c, d, io, st);
+    if (ea != hipSuccess) return ea;
+  } else if (c.alloc_impl == 2) {
+    const hipError_t ea = launch_alloc_scan(c, d, io, st);
+    if (ea != hipSuccess) return ea;
   } else {
-    if (c.alloc_sort) hipLaunchKernelGGL(alloc_sort_kernel, dim3(1), dim3(1024), 0, st, d);
+    if (c.alloc_sort) hipLaunchKernelGGL(alloc_sort_kernel, dim3(1), dim3(1024), 0, st, d, io);
     hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
   }
   const size_t lds_c = (size_t)c.W * BS * sizeof(double) + (c.obs_stage ? (size_t)c.W * BS * (c.L + 1) * sizeof(float) : 0);

@@ -234,6 +234,141 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   }
 }
 
+// Fused Linear -> ReLU -> Linear (one hidden layer: the reference's IPPO actor / critic [256],
+// config_files/algorithms/ippo.yaml:46,52; the test configs' [128] and [1024] heads): the hidden
+// layer is produced TB tiles of 32 units at a time (layer 1 exactly as in mlp3_relu_kernel) and
+// folded into the output accumulators as soon as it is final, so any hidden size up to 1024 runs
+// with 16 TB accumulator registers. VKO > 0: output layer on the VALU (weights in LDS), else on
+// the MFMA (fragments from L2, KO <= 32 rows).
+template <int TB, int WPE, int VKO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mlp2_relu_kernel(
+    const float* __restrict__ x, int64_t n, int L, int KS1, int NT1, const float4* __restrict__ w1p,
+    const float* __restrict__ b1, const float4* __restrict__ w3p, const float* __restrict__ b3, int KO,
+    float* __restrict__ out, const float* __restrict__ pre1, int grp, int prio) {
+  static_assert(VKO >= 0 && VKO <= 8, "VALU output layer: at most 8 outputs");
+  if (prio) __builtin_amdgcn_s_setprio(3);
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  extern __shared__ float4 w3d[];  // VALU output layer: [NT1 * 16][2][8 floats]
+  if constexpr (VKO > 0) {
+    for (int i = threadIdx.x; i < NT1 * 16 * 2 * 2; i += blockDim.x) w3d[i] = w3p[i];
+    __syncthreads();
+  }
+  if (tile * 32 >= n) return;  // wave-uniform
+  const int64_t j = tile * 32 + (lane & 31);
+  const bool jv = j < n;
+  const int M4 = (KS1 + 3) / 4;
+  const float* xr = x + (jv ? j : 0) * (int64_t)L;
+  const float* pg = pre1 != nullptr ? pre1 + ((jv ? j : 0) / grp) * (int64_t)(NT1 * 32) : nullptr;
+  auto load_x = [&](int m4, float (&xv)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int m = m4 * 4 + i, k = h * KS1 + m;
+      xv[i] = (jv && m < KS1 && k < L) ? xr[k] : 0.0f;
+    }
+  };
+  mlp_f32x16 a3;
+  float o3[VKO > 0 ? VKO : 1];
+  if constexpr (VKO > 0) {
+#pragma unroll
+    for (int a = 0; a < VKO; a++) o3[a] = (h == 0 && a < KO) ? b3[a] : 0.0f;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int row = mfma_row(r, h);
+      a3[r] = row < KO ? b3[row] : 0.0f;
+    }
+  }
+  for (int g0 = 0; g0 < NT1; g0 += TB) {
+    mlp_f32x16 a1[TB];
+#pragma unroll
+    for (int t = 0; t < TB; t++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        float4 v = *reinterpret_cast<const float4*>(b1 + (g0 + t) * 32 + 8 * q + 4 * h);
+        if (pg != nullptr) {
+          const float4 u = *reinterpret_cast<const float4*>(pg + (g0 + t) * 32 + 8 * q + 4 * h);
+          v.x += u.x, v.y += u.y, v.z += u.z, v.w += u.w;
+        }
+        a1[t][4 * q] = v.x, a1[t][4 * q + 1] = v.y, a1[t][4 * q + 2] = v.z, a1[t][4 * q + 3] = v.w;
+      }
+    {
+      float xc[4], xn[4];
+      float4 wc[TB], wn[TB];
+      load_x(0, xc);
+#pragma unroll
+      for (int t = 0; t < TB; t++) wc[t] = w1p[((int64_t)(g0 + t) * M4) * 64 + lane];
+      for (int m4 = 0; m4 < M4; m4++) {
+        const bool more = m4 + 1 < M4;
+        if (more) {
+          load_x(m4 + 1, xn);
+#pragma unroll
+          for (int t = 0; t < TB; t++) wn[t] = w1p[((int64_t)(g0 + t) * M4 + m4 + 1) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < TB; t++) {
+          a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[t].x, xc[0], a1[t], 0, 0, 0);
+          a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[t].y, xc[1], a1[t], 0, 0, 0);
+          a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[t].z, xc[2], a1[t], 0, 0, 0);
+          a1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[t].w, xc[3], a1[t], 0, 0, 0);
+        }
+        if (more) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) xc[i] = xn[i];
+#pragma unroll
+          for (int t = 0; t < TB; t++) wc[t] = wn[t];
+        }
+      }
+    }
+    // output layer over this group's hidden units (ReLU applied as they are read)
+    if constexpr (VKO > 0) {
+#pragma unroll
+      for (int t = 0; t < TB; t++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const float hv = fmaxf(a1[t][r], 0.0f);
+          const int sidx = ((g0 + t) * 16 + r) * 2 + h;
+          const float4 wa = w3d[sidx * 2];
+          const float wv[4] = {wa.x, wa.y, wa.z, wa.w};
+          float wh[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (VKO > 4) {
+            const float4 wb = w3d[sidx * 2 + 1];
+            wh[0] = wb.x, wh[1] = wb.y, wh[2] = wb.z, wh[3] = wb.w;
+          }
+#pragma unroll
+          for (int a = 0; a < VKO; a++) o3[a] = fmaf(a < 4 ? wv[a] : wh[a - 4], hv, o3[a]);
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < TB; t++)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; r4++) {
+          const float4 wq = w3p[((int64_t)(g0 + t) * 4 + r4) * 64 + lane];
+          a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(wq.x, fmaxf(a1[t][r4 * 4 + 0], 0.0f), a3, 0, 0, 0);
+          a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(wq.y, fmaxf(a1[t][r4 * 4 + 1], 0.0f), a3, 0, 0, 0);
+          a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(wq.z, fmaxf(a1[t][r4 * 4 + 2], 0.0f), a3, 0, 0, 0);
+          a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(wq.w, fmaxf(a1[t][r4 * 4 + 3], 0.0f), a3, 0, 0, 0);
+        }
+    }
+  }
+  if constexpr (VKO > 0) {
+#pragma unroll
+    for (int a = 0; a < VKO; a++) o3[a] += __shfl_xor(o3[a], 32);
+    if (jv && h == 0) {
+#pragma unroll
+      for (int a = 0; a < VKO; a++)
+        if (a < KO) out[j * KO + a] = o3[a];
+    }
+  } else if (jv) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int row = mfma_row(r, h);
+      if (row < KO) out[j * KO + row] = a3[r];
+    }
+  }
+}
+
 // layer-2 output tiles per pass at 256 hidden units: 8 (all of H2 at once, 1 wave per SIMD, default:
 // 1.547 vs 1.610 ms per rollout step) or 4 (<= 256 VGPRs, 2 waves per SIMD; MSC_MLP_P8=4, A/B)
 static int mlp_p8() {
@@ -287,6 +422,8 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
     case 8: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 8); break;               \
     default: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 0); break;              \
   }
+  // H1 held whole in registers, H2 in passes of P tiles; (NT1, P) sets the register budget
+  // (16 NT1 + 24 P + ~48 per lane) and with it the waves per SIMD
   if (H1 == 256 && H2 == 256) {
     if (mlp_p8() == 8) MSC_MLP_VKO(8, 8, 8, 1)
     else if (mlp_p8() == 4) MSC_MLP_VKO(8, 8, 4, 2)
@@ -295,11 +432,76 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
     MSC_MLP_VKO(4, 4, 4, 2)
   } else if (H1 == 64 && H2 == 64) {
     MSC_MLP_VKO(2, 2, 2, 4)
+  } else if (H1 == 64 && H2 == 128) {
+    MSC_MLP_VKO(2, 4, 2, 4)
+  } else if (H1 == 64 && H2 == 256) {
+    MSC_MLP_VKO(2, 8, 2, 4)
+  } else if (H1 == 64 && H2 == 512) {
+    MSC_MLP_VKO(2, 16, 2, 4)
+  } else if (H1 == 128 && H2 == 64) {
+    MSC_MLP_VKO(4, 2, 2, 2)
+  } else if (H1 == 128 && H2 == 256) {
+    MSC_MLP_VKO(4, 8, 4, 2)
+  } else if (H1 == 128 && H2 == 512) {
+    MSC_MLP_VKO(4, 16, 4, 2)
+  } else if (H1 == 256 && H2 == 64) {
+    MSC_MLP_VKO(8, 2, 2, 2)
+  } else if (H1 == 256 && H2 == 128) {
+    MSC_MLP_VKO(8, 4, 4, 2)
+  } else if (H1 == 256 && H2 == 512) {
+    MSC_MLP_VKO(8, 16, 8, 1)
+  } else if (H1 == 512 && H2 == 64) {
+    MSC_MLP_VKO(16, 2, 2, 1)
+  } else if (H1 == 512 && H2 == 128) {
+    MSC_MLP_VKO(16, 4, 4, 1)
+  } else if (H1 == 512 && H2 == 256) {
+    MSC_MLP_VKO(16, 8, 4, 1)
+  } else if (H1 == 512 && H2 == 512) {
+    MSC_MLP_VKO(16, 16, 4, 1)
   } else {
     return hipErrorInvalidValue;
   }
 #undef MSC_MLP_VKO
 #undef MSC_MLP_LAUNCH
+  return hipGetLastError();
+}
+
+// one hidden layer of H1 = 32 NT1 units (NT1 <= 32): TB tiles per group, the largest power of two
+// <= 8 dividing NT1
+bool mlp2_supported(int H1) { return H1 >= 32 && H1 <= 1024 && H1 % 32 == 0; }
+
+hipError_t launch_mlp2_relu(const float* x, int64_t n, int L, int H1, int KO, const float* w1p, const float* b1,
+                            const float* w3p, const float* b3, float* out, const float* pre1, int grp, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (!mlp2_supported(H1)) return hipErrorInvalidValue;
+  const int KS1 = (L + 1) / 2, NT1 = H1 / 32;
+  const int TB = NT1 % 8 == 0 ? 8 : NT1 % 4 == 0 ? 4 : NT1 % 2 == 0 ? 2 : 1;
+  const int64_t tiles = (n + 31) / 32;
+  const dim3 grid((unsigned)((tiles + 3) / 4)), block(256);
+  const float4* w1 = reinterpret_cast<const float4*>(w1p);
+  const float4* w3 = reinterpret_cast<const float4*>(w3p);
+  const int vko = mlp3_valu_outputs(KO);
+  const size_t lds = vko > 0 ? (size_t)NT1 * 16 * 2 * 2 * sizeof(float4) : 0;
+#define MSC_MLP2_LAUNCH(TBV, WPE, VKO)                                                                              \
+  hipLaunchKernelGGL((mlp2_relu_kernel<TBV, WPE, VKO>), grid, block, lds, st, x, n, L, KS1, NT1, w1, b1, w3, b3, KO, \
+                     out, pre1, grp, mlp_prio())
+#define MSC_MLP2_VKO(TBV, WPE)                  \
+  switch (vko) {                                \
+    case 1: MSC_MLP2_LAUNCH(TBV, WPE, 1); break; \
+    case 2: MSC_MLP2_LAUNCH(TBV, WPE, 2); break; \
+    case 4: MSC_MLP2_LAUNCH(TBV, WPE, 4); break; \
+    case 5: MSC_MLP2_LAUNCH(TBV, WPE, 5); break; \
+    case 8: MSC_MLP2_LAUNCH(TBV, WPE, 8); break; \
+    default: MSC_MLP2_LAUNCH(TBV, WPE, 0); break; \
+  }
+  switch (TB) {
+    case 8: MSC_MLP2_VKO(8, 2) break;
+    case 4: MSC_MLP2_VKO(4, 4) break;
+    case 2: MSC_MLP2_VKO(2, 4) break;
+    default: MSC_MLP2_VKO(1, 4) break;
+  }
+#undef MSC_MLP2_VKO
+#undef MSC_MLP2_LAUNCH
   return hipGetLastError();
 }
 

@@ -159,6 +159,14 @@ class VecInventoryEnv:
         abi.check(abi.lib().msc_env_read_timing(self._h, C.byref(d), C.byref(s), C.byref(nd), C.byref(ns)))
         return {"demand_ms": d.value, "step_ms": s.value, "n_demand": nd.value, "n_step": ns.value}
 
+    def read_timing_ea(self) -> Dict[str, float]:
+        """Episode-ahead demand (msc_env_read_timing_ea): mean device ms of the timed episode
+        generation launches, their count, slots per env (0: off) and whether the current episode
+        reads a generated slot."""
+        ms, n, slots, act = C.c_double(), C.c_int64(), C.c_int32(), C.c_int32()
+        abi.check(abi.lib().msc_env_read_timing_ea(self._h, C.byref(ms), C.byref(n), C.byref(slots), C.byref(act)))
+        return {"ea_ms": ms.value, "n_ea": n.value, "slots": slots.value, "active": bool(act.value)}
+
     def alloc_info(self) -> Dict[str, torch.Tensor]:
         """Device buffers for msc_step_info (the reference's collect_step_info dict)."""
         E, W, K, R = self.n_envs, self.W, self.K, self.R

@@ -17,26 +17,36 @@ REW_ATOL = 1e-6
 
 
 def _set_alloc(monkeypatch, param):
-    impl, _, opt = param.partition("_")
-    monkeypatch.setenv("MSC_ALLOC_IMPL", impl[:4] if impl != "group" else "group")
+    # "<impl>[_<opt>...]": impl lane / lane2 / lane4 (one env per lane, 1 / 2 / 4 lanes per env),
+    # group (one env per lane group), scan (one env per wave, prefix scan over the cost ranking);
+    # opts sorted / unsorted (group kernel's visiting order), ea0 / ea1 (episode-ahead demand off /
+    # on; default: on for the scan kernel, the library's choice for group, off for lane)
+    impl, *opts = param.split("_")
+    monkeypatch.setenv("MSC_ALLOC_IMPL", "lane" if impl.startswith("lane") else impl)
     monkeypatch.setenv("MSC_ALLOC_LPE", impl[4:] if impl.startswith("lane") and impl[4:] else "0")
     # group kernel: envs visited in descending order of their order count (default for empirical
     # demand), forced on ("sorted") or off ("unsorted")
-    if opt:
-        monkeypatch.setenv("MSC_ALLOC_SORT", "1" if opt == "sorted" else "0")
+    sort = [o for o in opts if o in ("sorted", "unsorted")]
+    if sort:
+        monkeypatch.setenv("MSC_ALLOC_SORT", "1" if sort[0] == "sorted" else "0")
     else:
         monkeypatch.delenv("MSC_ALLOC_SORT", raising=False)
+    ea = "0" if "ea0" in opts or impl.startswith("lane") else "1" if ("ea1" in opts or impl == "scan") else None
+    if ea is None:
+        monkeypatch.delenv("MSC_EA", raising=False)
+    else:
+        monkeypatch.setenv("MSC_EA", ea)
 
 
-@pytest.fixture(params=["lane", "group", "group_sorted"])
+@pytest.fixture(params=["lane", "group", "group_sorted", "scan", "scan_ea0"])
 def alloc_impl(request, monkeypatch):
-    # both phase-B allocation kernels (one env per lane / one env per lane group) against the same
-    # references; msc_env_create picks by shape otherwise (small test batches would get the group one)
+    # every phase-B allocation kernel (one env per lane / per lane group / per wave) against the same
+    # references, with and without episode-ahead demand; msc_env_create picks by shape otherwise
     _set_alloc(monkeypatch, request.param)
     return request.param
 
 
-@pytest.fixture(params=["lane", "lane2", "lane4", "group", "group_sorted", "group_unsorted"])
+@pytest.fixture(params=["lane", "lane2", "lane4", "group", "group_sorted", "group_unsorted_ea1", "scan", "scan_ea0"])
 def alloc_impl_lpe(request, monkeypatch):
     # as alloc_impl, plus the lane kernel's 2 / 4 lanes-per-env forms (A/B; >= 8 warehouses)
     _set_alloc(monkeypatch, request.param)
@@ -453,3 +463,68 @@ def test_empirical_trace_demand_vs_oracle(W, R, lost):
     trace = make_synthetic_trace(R, 5, 25, orders_per_step=(200, 1000) if R > 64 else (2, 12), seed=W)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True, "demand_trace": trace})
     _lockstep(spec, 96, 14, seed=4, check_every=3)
+
+
+def test_episode_ahead_equals_sequential(monkeypatch):
+    # episode-ahead demand (whole future episodes drawn on a side stream)
+    # against per-step sequential demand: identical observations, rewards and reported state
+    # (PCG64 demand stream included) across episode boundaries, save/load in the middle of a
+    # generated episode, a full reset mid-episode, a masked reset and episode-counter rewrites
+    monkeypatch.setenv("MSC_EA", "1")
+    monkeypatch.setenv("MSC_EA_SLOTS", "4")
+    monkeypatch.setenv("MSC_ALLOC_IMPL", "scan")
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=6)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    E = 192
+    a, b = _vec(spec, E, base_seed=31), _vec(spec, E, base_seed=31)
+    b.set_pipelining(False)
+    a.reset(), b.reset()
+    rng = np.random.default_rng(12)
+    acts = [torch.from_numpy(rng.uniform(-1, 1, (E, 8, 5)).astype(np.float32)).cuda() for _ in range(90)]
+    a.set_timing(200)
+    seen_active = False
+    for t, act in enumerate(acts):
+        if t == 27:  # step 3 of a generated episode
+            assert a.read_timing_ea()["active"]
+            blob = a.save_state()
+            first = [a.step(x)[0].clone() for x in acts[27:30]]
+            a.load_state(blob)
+            second = [a.step(x)[0].clone() for x in acts[27:30]]
+            for x, y in zip(first, second):
+                assert torch.equal(x, y)
+            a.load_state(blob)
+        if t == 40:
+            a.reset(), b.reset()
+        if t == 58:
+            cnt = np.arange(E, dtype=np.int32) % 3
+            a.set_episode_counters(cnt), b.set_episode_counters(cnt)
+        if t == 75:
+            m = torch.zeros(E, dtype=torch.uint8, device="cuda")
+            m[::5] = 1
+            a.reset(mask=m), b.reset(mask=m)
+        oa = a.step(act)[0].clone()
+        ob = b.step(act)[0].clone()
+        assert torch.equal(oa, ob), f"step {t}"
+        assert torch.equal(a.rewards, b.rewards), f"step {t}"
+        seen_active |= a.read_timing_ea()["active"]
+        if t % 4 == 1:
+            sa, sb = a.read_state(), b.read_state()
+            for k in ("rng", "inventory", "timestep", "episode_counter"):
+                assert np.array_equal(sa[k], sb[k]), f"{k} at step {t}"
+    assert seen_active
+    tm = a.read_timing_ea()
+    assert tm["slots"] == 4 and tm["n_ea"] > 0 and tm["ea_ms"] > 0
+    a.check()
+    b.check()
+
+
+@pytest.mark.parametrize("E", [1, 63, 1000])
+def test_scan_allocator_vs_oracle_sizes(monkeypatch, E):
+    # the scan allocator (4 envs per block; a partial last block) and episode-ahead demand at odd
+    # env counts against the oracle, with max_splits limiting the warehouses per order
+    monkeypatch.setenv("MSC_ALLOC_IMPL", "scan")
+    monkeypatch.setenv("MSC_EA", "1")
+    cfg = make_synthetic_env_config(6, 20, 4, episode_length=5)
+    cfg["components"]["demand_allocator"]["params"]["max_splits"] = 1
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, E, 17, seed=E, check_every=2)

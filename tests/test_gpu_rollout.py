@@ -184,3 +184,93 @@ def test_gaussian_sample_kernel_matches_torch_formula():
     torch.testing.assert_close(act, a, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(logp, lp, rtol=1e-5, atol=1e-5)
     assert torch.equal(clipped, act.clamp(-1.0, 1.0))
+
+
+@pytest.mark.parametrize("L,hidden,KO,n", [
+    (34, [256], 5, 32768),        # IPPO actor (config_files/algorithms/ippo.yaml:46): one hidden layer
+    (34, [256], 1, 4099),         # IPPO critic on local obs (:52)
+    (306, [1024], 1, 1000),       # the MAPPO test config's [1024] critic head over the flat obs
+    (42, [128], 1, 77),           # the IPPO test config's [128] critic
+    (13, [96], 7, 65),            # hidden 3 tiles of 32 (one tile per group), 7 outputs
+    (34, [160], 17, 300),         # 5 tiles, MFMA output layer (> 8 outputs)
+    (34, [256, 128], 5, 2048),    # unequal two-layer forms
+    (34, [128, 256], 1, 513),
+    (34, [64, 512], 5, 700),
+    (34, [512, 64], 5, 700),
+    (34, [512, 512], 32, 257),
+])
+def test_fused_mlp_forms_match_torch_layers(L, hidden, KO, n):
+    # msc_mlp2_relu_forward / msc_mlp3_relu_forward against the torch fp32 layer sequence of the
+    # same MLP (tolerance 2e-5 abs / rel), and the weight pack follows in-place updates
+    from marlsc.mlp import fused_layers, mlp3_forward
+    from marlsc.rollout import MLP
+    torch.manual_seed(L + sum(hidden) + KO)
+    mlp = MLP(L, KO, {"hidden_sizes": hidden}).cuda()
+    mods = list(mlp)
+    assert fused_layers(mods) == len(hidden) + 1
+    x = torch.randn(n, L, device="cuda")
+
+    def ref():
+        y = x
+        for m in mods:
+            y = m(y)
+        return y
+    with torch.no_grad():
+        torch.testing.assert_close(mlp3_forward(mods, x), ref(), rtol=2e-5, atol=2e-5)
+        mods[0].weight.mul_(-0.75)
+        torch.testing.assert_close(mlp3_forward(mods, x), ref(), rtol=2e-5, atol=2e-5)
+
+
+def test_fused_mlp_rejects_unsupported_shapes():
+    from marlsc.mlp import fused_layers
+    from marlsc.rollout import MLP
+    assert fused_layers(list(MLP(34, 5, {"hidden_sizes": [100]}))) == 0     # not a multiple of 32
+    assert fused_layers(list(MLP(34, 5, {"hidden_sizes": [96, 96]}))) == 0  # two-layer sizes: 64..512 powers of 2
+    assert fused_layers(list(MLP(2000, 5, {"hidden_sizes": [256]}))) == 0   # more than 1024 inputs
+    assert fused_layers(list(MLP(34, 40, {"hidden_sizes": [256]}))) == 0    # more than 32 outputs
+    assert fused_layers(list(MLP(34, 5, {"hidden_sizes": [64, 64, 64]}))) == 0
+
+
+def test_fused_mappo_test_critic_1024_matches_split_layers():
+    # the reference's mappo_test.yaml critic [1024] over local_w || global, through the one-hidden-
+    # layer kernel with the per-env global block as pre1
+    from marlsc.rollout import MLP, split_global_mlp
+    torch.manual_seed(5)
+    W, L = 8, 34
+    critic = MLP(L * (1 + W), 1, {"hidden_sizes": [1024]}).cuda()
+    x = torch.randn(300, W, L, device="cuda")
+    with torch.no_grad():
+        fused = split_global_mlp(critic, x)
+    full = critic(torch.cat([x, x.reshape(300, 1, W * L).expand(300, W, W * L)], dim=-1)).detach()
+    torch.testing.assert_close(fused, full, rtol=2e-5, atol=2e-5)
+
+
+def test_multi_lane_rollout_after_weight_update_uses_fresh_packs():
+    # with two rollout lanes (two HIP streams) the fused-MLP pack rebuilt after a weight
+    # update on one lane's stream must be ordered before the other lane's use: every stored value
+    # equals the critic on the stored observation with the updated weights
+    from marlsc import make_synthetic_env_config
+    from marlsc.rollout import ActorCritic, RolloutCollector, RolloutConfig
+    from marlsc.spec import EnvSpec
+    from marlsc.vec_env import VecInventoryEnv
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=9)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    lanes = [VecInventoryEnv(None, 2048, spec=spec, device=0, base_seed=7, env_index_offset=0),
+             VecInventoryEnv(None, 2048, spec=spec, device=0, base_seed=7, env_index_offset=2048)]
+    for x in lanes:
+        x.reset()
+    torch.manual_seed(1)
+    rc = RolloutConfig(critic_obs_type="local", critic={"hidden_sizes": [256, 256]})
+    m = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
+    col = RolloutCollector(lanes, m, 6, seed=3)
+    col.collect(normalize=False)
+    for it in range(3):
+        with torch.no_grad():  # an optimizer step: in-place parameter updates
+            for p in m.parameters():
+                p.add_(0.01 * torch.randn_like(p))
+        col.collect(normalize=False)
+        torch.cuda.synchronize()
+        with torch.enable_grad():  # torch layers (no fused kernel) as the reference
+            for t in (0, 3, 5):
+                ref = m.critic(col.obs[t]).squeeze(-1).detach()
+                torch.testing.assert_close(col.values[t], ref, rtol=2e-5, atol=2e-5)
