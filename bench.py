@@ -156,8 +156,10 @@ def c2_line(args, rank: int):
     pool = [torch.rand((E, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
     env.reset()
     T = spec.episode_length
-    steps = max(args.steps, 5 * T)
-    warm = 3 * T  # episode 0 of the episode-ahead snapshot draws per step; later ones read slots
+    steps = max(args.steps, 10 * T)
+    # episode 0 of the episode-ahead snapshot draws its demand per step while the first S - 1
+    # episodes are generated; the slots refill in steady state after a few episodes
+    warm = 10 * T
     dt, tm = time_env(env, pool, steps, warm, 1)
     rc = RolloutConfig.from_algorithm_config(algo)
     torch.manual_seed(0)

@@ -35,16 +35,32 @@
 
 namespace msc {
 
+#ifdef MSC_PROF
+// in-kernel cycle accounting (profiling build: make prof -> libmarlsc_prof.so, tools/prof_scan.py)
+__device__ unsigned long long g_prof_scan[8];
+#define SPROF(v) unsigned long long v = 0
+#define SPROF_T(v) const unsigned long long v = (unsigned long long)clock64()
+#define SPROF_ADD(v, x) (v) += (x)
+#define SPROF_NOW() ((unsigned long long)clock64())
+#define SPROF_FLUSH(i, v) \
+  if (lane == 0) atomicAdd(&g_prof_scan[i], (v))
+#else
+#define SPROF(v)
+#define SPROF_T(v)
+#define SPROF_ADD(v, x)
+#define SPROF_NOW() 0ull
+#define SPROF_FLUSH(i, v)
+#endif
+
 constexpr int SC_WAVES = 4;  // envs (waves) per block
 constexpr int SC_WIN = 64;   // orders ranked per window (one per lane)
 #ifndef MSC_SC_PRIO
 #define MSC_SC_PRIO 3  // s_setprio: the step chain is the critical path next to the demand generator
 #endif
 
-// LDS per wave: the window's order records and their packed ranks, epilogue scratch
+// LDS per wave: the window's order records, epilogue scratch
 struct ScWaveLds {
   uint4 rec[SC_WIN];
-  uint2 hdr[SC_WIN];  // {region, rho}
   int32_t iscr[64];
   double dscr[64];
 };
@@ -100,14 +116,23 @@ __device__ __forceinline__ uint32_t rec_field(const uint4& v, int h) {  // h: co
   return (h & 1) ? (w >> 16) : (w & 0xffffu);
 }
 
-template <int K, int GW>
+// Orders of one region with the same cost ranking form a batch: greedy fills of consecutive orders
+// over one ranking are the fills of their running demand total, so order k of a batch takes
+//     f_{k,p,s} = a_k - a_{k-1},  a_k = min(inv_{p,s}, max(0, D_{k,s} - sum_{q<p} inv_{q,s})),
+// D_k = d_1 + ... + d_k, and the whole batch needs one permute, one scan and one bpermute; per order
+// only the contributing-warehouse flags (shipment counts) and the lost-order test remain, a few
+// VALU instructions without any LDS round trip. (With max_splits limiting the warehouses per order
+// every order is its own batch.)
+template <int K, int GW, bool TAB>
 __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   static_assert(K * GW <= 64 && K <= 6, "lane = s * GW + w; one uint4 per order record");
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int W = c.W, R = c.R, WK = W * K;
   const int64_t E = c.E;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // (the wave index through readfirstlane: the compiler's divergence analysis would otherwise treat
+  // the env and everything derived from it -- order counts, loop bounds -- as per-lane values)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t e = (int64_t)blockIdx.x * SC_WAVES + wave;
   const int sk = lane / GW, w = lane % GW;  // this lane's SKU and warehouse (its rank p in rank space)
   const bool lv = sk < K && w < W;
@@ -116,23 +141,29 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   if (MSC_SC_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SC_PRIO);
 
   extern __shared__ __attribute__((aligned(16))) char sc_lds[];
-  const bool tab = sc_tab_bytes(R, GW) <= SC_TAB_MAX;
   double2* Ltab = reinterpret_cast<double2*>(sc_lds);  // [w][R | 1] {of, ov}
-  ScWaveLds* Lw = reinterpret_cast<ScWaveLds*>(sc_lds + (tab ? sc_tab_bytes(R, GW) : 0)) + wave;
+  int32_t* Lcl = reinterpret_cast<int32_t*>(sc_lds + (TAB ? sc_tab_bytes(R, GW) : 0));  // [R] closest warehouse
+  ScWaveLds* Lw = reinterpret_cast<ScWaveLds*>(Lcl + ((R + 3) & ~3)) + wave;
   const int RS = R | 1;
-  if (tab) {
+  if constexpr (TAB) {
     for (int i = threadIdx.x; i < R * GW; i += blockDim.x) {
       const int ww = i / R, r = i % R;
       Ltab[ww * RS + r] = ww < W ? make_double2(c.ofT[r * W + ww], c.ovT[r * W + ww]) : make_double2(0.0, 0.0);
     }
   }
+  for (int i = threadIdx.x; i < R; i += blockDim.x) Lcl[i] = c.closest[i];
   __syncthreads();  // the only block barrier: waves (envs) are independent from here on
   if (e >= E) return;
   auto tab_at = [&](int r, int ww) -> double2 {
-    if (tab) return Ltab[ww * RS + r];
-    const int wc = ww < W ? ww : W - 1;
-    return make_double2(gp(c.ofT)[r * W + wc], gp(c.ovT)[r * W + wc]);
+    if constexpr (TAB) {
+      return Ltab[ww * RS + r];
+    } else {
+      const int wc = ww < W ? ww : W - 1;
+      return make_double2(gp(c.ofT)[r * W + wc], gp(c.ovT)[r * W + wc]);
+    }
   };
+  // LDS written by some lanes and read by others of the same wave: a wave's LDS instructions execute
+  // in order, so only the compiler must not move the accesses
   auto wave_sync = [] {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -151,75 +182,89 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   const double skw_me = sk < K ? c.skw[sk] : 0.0;
   const double pen_me = sk < K ? (pps ? c.pen[sk] : c.pen_scalar) : 0.0;
   const int myhome = w < W ? c.home_of[w] : -1;
+  const bool lastp = w == GW - 1;  // the lane of the last rank of its SKU (holds the SKU's total)
 
   const int64_t gi = (int64_t)(w * K + sk) * E + e;  // this lane's [w*K + s][E] state index
   int inv = lv ? s.inv[gi] : 0;
   const int inv0 = inv;
   int qsr = 0, cnt = 0, u = 0, dsum = 0, lost_cnt = 0;
-  double lost = 0.0, ofix = 0.0, ovar = 0.0, of_me = 0.0, ov_me = 0.0;
+  // ofix: sum_r count * fixed; ovacc: sum_r shipped(w, r, s) * variable (the SKU weights applied once
+  // at the end: out_var_w = sum_s w_s ovacc_s, reward_calculator.py:141-142 reordered)
+  double lost = 0.0, ofix = 0.0, ovacc = 0.0, of_me = 0.0, ov_me = 0.0;
   int inc_h = 0, shh_h = 0;
   bool home_done = false;
   int cur = -1;
+  uint32_t cur_rho = 0xFFFFFFFFu;
 
   const OrderSrc o = order_src<1>(c, s, io, e);
-  const int n = o.n;
+  const int n = __builtin_amdgcn_readfirstlane(o.n);
   const MSC_GLOBAL uint4* src = gp(o.src);
   if (dbg && lane == 0 && info.n_orders) info.n_orders[e] = n;
 
   // region epilogue: lost sales, outbound cost, home features of region r (uniform)
   auto epilogue = [&](int r) {
-    const int ug = __shfl(u, sk * GW + GW - 1);  // the SKU's unfulfilled demand (kept by its last rank lane)
-    Lw->iscr[lane] = qsr;
-    if (w == GW - 1) Lw->dscr[sk] = (double)ug;
-    wave_sync();
-    int acc = 0;       // units this warehouse shipped to the region (shipment_quantities[w, r])
-    double wsum = 0.0; // their weight (outbound_shipment_weights[w, r], SKU order: numpy's for K < 8)
-#pragma unroll
-    for (int j = 0; j < K; j++) {
-      const int q = Lw->iscr[j * GW + w];
-      acc += q;
-      wsum += (double)q * skw[j];
-    }
-    if (lost_cnt > 0) {
-      double wt = 0.0;
-      const int tot = sc_group_reduce<GW>(acc, [](int a, int b) { return a + b; });
-      if (lost_type == MSC_LOST_COST) {  // softmax(-(of * lost_orders + ov * lost_weight) / alpha)
-        double lw = 0.0;                 // unfulfilled[r] . sku_weights
-#pragma unroll
-        for (int j = 0; j < K; j++) lw += Lw->dscr[j] * skw[j];
-        const double lg = w < W ? -(of_me * (double)lost_cnt + ov_me * lw) / alpha : -INFINITY;
-        const double mx = sc_group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
-        const double ex = w < W ? exp(lg - mx) : 0.0;
-        wt = w < W ? ex / sc_group_np_sum<GW>(ex, W) : 0.0;
-      } else if (lost_type == MSC_LOST_SHIPMENT && tot > 0) {
-        wt = acc > 0 ? (double)acc / (double)tot : 0.0;
-      } else {  // closest warehouse (shipment with nothing shipped falls back to it)
-        wt = w == c.closest[r] ? 1.0 : 0.0;
-      }
-      if (wt != 0.0) lost += wt * (double)ug;
-    }
     ofix += (double)cnt * of_me;
-    ovar += wsum * ov_me;
+    ovacc += (double)qsr * ov_me;
     if (r == myhome) {
       inc_h = dsum;
       shh_h = qsr;
       home_done = true;
     }
-    if (dbg) {
-      if (w == 0 && sk < K) {
-        if (info.demand_per_region) info.demand_per_region[(e * R + r) * K + sk] = dsum;
-        if (info.unfulfilled_demands) info.unfulfilled_demands[(e * R + r) * K + sk] = ug;
+    if (lost_cnt > 0 || dbg) {
+      const int ug = __shfl(u, sk * GW + GW - 1);  // the SKU's unfulfilled demand (kept by its last rank lane)
+      if (lost_cnt > 0) {
+        double wt = 0.0;
+        if (lost_type == MSC_LOST_CLOSEST) {
+          wt = w == Lcl[r] ? 1.0 : 0.0;
+        } else {
+          Lw->iscr[lane] = qsr;
+          if (lastp) Lw->dscr[sk] = (double)ug;
+          wave_sync();
+          int acc = 0;  // units this warehouse shipped to the region (shipment_quantities[w, r])
+#pragma unroll
+          for (int j = 0; j < K; j++) acc += Lw->iscr[j * GW + w];
+          if (lost_type == MSC_LOST_COST) {  // softmax(-(of * lost_orders + ov * lost_weight) / alpha)
+            double lw = 0.0;                 // unfulfilled[r] . sku_weights
+#pragma unroll
+            for (int j = 0; j < K; j++) lw += Lw->dscr[j] * skw[j];
+            const double lg = w < W ? -(of_me * (double)lost_cnt + ov_me * lw) / alpha : -INFINITY;
+            const double mx = sc_group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
+            const double ex = w < W ? exp(lg - mx) : 0.0;
+            wt = w < W ? ex / sc_group_np_sum<GW>(ex, W) : 0.0;
+          } else {  // shipment shares; nothing shipped: the closest warehouse
+            const int tot = sc_group_reduce<GW>(acc, [](int a, int b) { return a + b; });
+            wt = tot > 0 ? (acc > 0 ? (double)acc / (double)tot : 0.0) : (w == Lcl[r] ? 1.0 : 0.0);
+          }
+          if (dbg && sk == 0 && w < W) {
+            if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] = acc;
+          }
+          wave_sync();  // iscr / dscr are rewritten by the next epilogue
+        }
+        if (wt != 0.0) lost += wt * (double)ug;
       }
-      if (lane == 0 && info.lost_order_counts) info.lost_order_counts[e * R + r] = lost_cnt;
-      if (lv) {
-        if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] = qsr;
-        if (sk == 0 && info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] = cnt;
-        if (sk == 0 && info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] = acc;
+      if (dbg) {
+        if (w == 0 && sk < K) {
+          if (info.demand_per_region) info.demand_per_region[(e * R + r) * K + sk] = dsum;
+          if (info.unfulfilled_demands) info.unfulfilled_demands[(e * R + r) * K + sk] = ug;
+        }
+        if (lane == 0 && info.lost_order_counts) info.lost_order_counts[e * R + r] = lost_cnt;
+        if (lv) {
+          if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] = qsr;
+          if (sk == 0 && info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] = cnt;
+        }
+        if (info.shipment_quantities && !(lost_cnt > 0 && lost_type != MSC_LOST_CLOSEST)) {
+          Lw->iscr[lane] = qsr;
+          wave_sync();
+          int acc = 0;
+#pragma unroll
+          for (int j = 0; j < K; j++) acc += Lw->iscr[j * GW + w];
+          if (sk == 0 && w < W) info.shipment_quantities[(e * W + w) * R + r] = acc;
+          wave_sync();
+        }
       }
     }
     qsr = cnt = u = dsum = 0;
     lost_cnt = 0;
-    wave_sync();  // iscr / dscr are rewritten by the next epilogue
   };
 
   // order ranks (demand_allocator.py:167-173): 4-bit rank of warehouse w at bits 4w (stable order:
@@ -248,6 +293,12 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   };
 
   const int fi = sk < K ? 1 + sk : 7;  // this lane's 16-bit field of a record (field 7 is 0: K <= 6)
+  SPROF(p_tot);
+  SPROF(p_rank);
+  SPROF(p_epi);
+  SPROF(n_epi);
+  SPROF(n_bat);
+  SPROF_T(t_begin);
   uint4 nxt = lane < n ? gload4(src, o.base + (int64_t)lane * o.nstep) : make_uint4(0u, 0u, 0u, 0u);
   for (int o0 = 0; o0 < n; o0 += SC_WIN) {
     const int nw = n - o0 < SC_WIN ? n - o0 : SC_WIN;
@@ -256,59 +307,107 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       const int oi = o0 + SC_WIN + lane;
       nxt = oi < n ? gload4(src, o.base + (int64_t)oi * o.nstep) : make_uint4(0u, 0u, 0u, 0u);
     }
+    SPROF_T(t_r0);
+    // this lane's order (o0 + lane): region, ranking; batch / region starts against the previous order
+    const int rg = (int)(rv.x & 0xffffu);
     const uint32_t rho = lane < nw ? rank_of(rv) : 0u;
+    int rg_prev = __shfl_up(rg, 1);
+    uint32_t rho_prev = (uint32_t)__shfl_up((int)rho, 1);
+    if (lane == 0) {
+      rg_prev = cur;
+      rho_prev = cur_rho;
+    }
+    const bool inw = lane < nw;
+    const uint64_t rstart = __ballot(inw && rg != rg_prev);
+    const uint64_t bstart = split ? __ballot(inw) : __ballot(inw && (rg != rg_prev || rho != rho_prev));
     Lw->rec[lane] = rv;
-    Lw->hdr[lane] = make_uint2(rv.x & 0xffffu, rho);
     wave_sync();
+    SPROF_ADD(p_rank, SPROF_NOW() - t_r0);
     const uint16_t* Lh = reinterpret_cast<const uint16_t*>(Lw->rec);
-    for (int i = 0; i < nw; i++) {
-      const uint2 hd = Lw->hdr[i];
-      const int d = Lh[i * 8 + fi];
-      const int r = __builtin_amdgcn_readfirstlane((int)hd.x);
-      const uint32_t rho_i = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.y);
-      if (r != cur) {  // region boundary (orders are region-major)
+    for (int i0 = 0; i0 < nw;) {
+      const uint64_t later = bstart & ~((2ull << i0) - 1ull);  // batch starts after i0
+      const int i1 = __builtin_amdgcn_readfirstlane(later ? (int)__builtin_ctzll(later) : nw);
+      const int r = __builtin_amdgcn_readlane(rg, i0);
+      const uint32_t rho_b = (uint32_t)__builtin_amdgcn_readlane((int)rho, i0);
+      int dn = Lh[i0 * 8 + fi];
+      if ((rstart >> i0) & 1ull) {  // region boundary (orders are region-major)
+        SPROF_T(t_e0);
         if (cur >= 0) epilogue(cur);
+        SPROF_ADD(p_epi, SPROF_NOW() - t_e0);
+        SPROF_ADD(n_epi, 1);
         cur = r;
         const double2 t = tab_at(r, w);
         of_me = t.x;
         ov_me = t.y;
       }
-      const int paddr = (sk * GW + (int)((rho_i >> (4 * w)) & 0xFu)) << 2;
+      cur_rho = rho_b;
+      SPROF_ADD(n_bat, 1);
+      const int paddr = (sk * GW + (int)((rho_b >> (4 * w)) & 0xFu)) << 2;
       const int x = __builtin_amdgcn_ds_permute(paddr, inv);  // rank space: inventory of the rank-w warehouse
       const int incl = group_scan<GW>(x, w);
-      const int need = d - (incl - x);  // demand left after the cheaper ranks
-      int f = need > 0 ? (need < x ? need : x) : 0;  // min(inv, max(0, d - prefix)): one v_med3
-      int rem;
-      if (split) {  // max_splits: only the first max_wh contributing ranks ship
-        uint32_t m = fold_groups<GW>(__ballot(f > 0));
-        if (__builtin_popcount(m) > maxwh) {
-          uint32_t keep = 0u;
-          for (int k = 0; k < maxwh; k++) {
-            keep |= m & (0u - m);
-            m &= m - 1u;
+      const int excl = incl - x;
+      int D = 0, a_prev = 0, cnt_r = 0;
+      for (int k = i0; k < i1; k++) {
+        const int d = dn;
+        if (k + 1 < i1) dn = Lh[(k + 1) * 8 + fi];
+        D += d;
+        const int need = D - excl;  // demand left after the cheaper ranks
+        const int a = need > 0 ? (need < x ? need : x) : 0;  // min(inv, max(0, D - prefix)): one v_med3
+        int f = a - a_prev;
+        a_prev = a;
+        if (split) {  // max_splits: only the first max_wh contributing ranks ship (a one-order batch)
+          uint32_t m = fold_groups<GW>(__ballot(f > 0));
+          if (__builtin_popcount(m) > maxwh) {
+            uint32_t keep = 0u;
+            for (int q = 0; q < maxwh; q++) {
+              keep |= m & (0u - m);
+              m &= m - 1u;
+            }
+            m = keep;
           }
-          m = keep;
+          f = ((m >> w) & 1u) ? f : 0;
+          a_prev = f;
+          cnt_r += (int)((m >> w) & 1u);
+          const int rem = d - group_scan<GW>(f, w);  // (this SKU's total in its last rank lane)
+          u += rem;
+          lost_cnt += __ballot(lastp && rem > 0) != 0 ? 1 : 0;
+        } else {
+          cnt_r += (int)((fold_groups<GW>(__ballot(f > 0)) >> w) & 1u);
+          // the order is short of SKU s <=> it asks for s and the running demand exceeds the stock
+          lost_cnt += __ballot(lastp && d > 0 && D > incl) != 0 ? 1 : 0;
         }
-        f = ((m >> w) & 1u) ? f : 0;
-        rem = d - group_scan<GW>(f, w);
-      } else {
-        rem = d - incl > 0 ? d - incl : 0;
+        dsum += d;
       }
-      const int fw = __builtin_amdgcn_ds_bpermute(paddr, f);  // back to the warehouse's lane
+      if (!split) u += D - incl > 0 ? D - incl : 0;  // the batch's unfulfilled units (last rank lane)
+      // total fill and contribution count of the rank back to its warehouse's lane, one bpermute:
+      // fill < 2^24 (<= 64 orders of < 2^16 units), count <= 64
+      const int back = __builtin_amdgcn_ds_bpermute(paddr, (cnt_r << 24) | a_prev);
+      const int fw = back & 0xFFFFFF;
       inv -= fw;
       qsr += fw;
-      dsum += d;
-      u += rem;  // (meaningful in the SKU's last rank lane: the order's unfulfilled demand)
-      cnt += (int)((fold_groups<GW>(__ballot(fw > 0)) >> w) & 1u);
-      lost_cnt += __ballot(w == GW - 1 && rem > 0) != 0 ? 1 : 0;
+      cnt += (int)((uint32_t)back >> 24);
+      i0 = i1;
     }
     wave_sync();  // the window is rewritten next
   }
+  SPROF_T(t_e1);
   if (cur >= 0) epilogue(cur);
+  SPROF_ADD(p_epi, SPROF_NOW() - t_e1);
+  SPROF_ADD(p_tot, SPROF_NOW() - t_begin);
+  SPROF_FLUSH(0, p_tot);
+  SPROF_FLUSH(1, p_rank);
+  SPROF_FLUSH(2, p_epi);
+  SPROF_FLUSH(3, n_epi);
+  SPROF_FLUSH(4, (unsigned long long)n);
+  SPROF_FLUSH(5, 1ull);
+  SPROF_FLUSH(6, n_bat);
 
-  // penalty (reward_calculator.py:134-137): (lost_sales * per-SKU cost or sku_weights * cost) summed
-  // over SKUs in order
+  // penalty (reward_calculator.py:134-137): (lost_sales * per-SKU cost, or * sku_weights * cost)
+  // summed over SKUs in order; outbound variable cost: sum over SKUs of sku_weight * ovacc
   Lw->dscr[lane] = pps ? lost * pen_me : (lost * skw_me) * pen_me;
+  Lw->rec[lane] = make_uint4(0u, 0u, 0u, 0u);
+  double* Lov = reinterpret_cast<double*>(Lw->rec);
+  Lov[lane] = skw_me * ovacc;
   wave_sync();
   if (lv) {
     s.inv[gi] = inv;
@@ -320,27 +419,37 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] = inv0 - inv;
     }
     if (sk == 0) {
-      double pen = 0.0;
+      double pen = 0.0, ovar = 0.0;
 #pragma unroll
-      for (int j = 0; j < K; j++) pen += Lw->dscr[j * GW + w];
+      for (int j = 0; j < K; j++) {
+        pen += Lw->dscr[j * GW + w];
+        ovar += Lov[j * GW + w];
+      }
       s.sc_pen[w * E + e] = pen;
       s.sc_out[w * E + e] = ofix + ovar;
     }
   }
 }
 
+static bool alloc_scan_tab(const EnvConst& c, int GW) { return sc_tab_bytes(c.R, GW) <= SC_TAB_MAX; }
 size_t alloc_scan_lds_bytes(const EnvConst& c) {
   const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : 8;
-  const size_t t = sc_tab_bytes(c.R, GW);
-  return (t <= SC_TAB_MAX ? t : 0) + SC_WAVES * sizeof(ScWaveLds);
+  return (alloc_scan_tab(c, GW) ? sc_tab_bytes(c.R, GW) : 0) + sizeof(int32_t) * ((c.R + 3) & ~3) +
+         SC_WAVES * sizeof(ScWaveLds);
 }
 bool alloc_scan_supported(int W, int K) { return W <= 8 && K <= 6; }
 
 template <int K>
 static void launch_scan_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   using KFn = void (*)(const DevEnv*, StepIO);
-  KFn f = c.W <= 2 ? (KFn)alloc_scan_kernel<K, 2> : c.W <= 4 ? (KFn)alloc_scan_kernel<K, 4> : (KFn)alloc_scan_kernel<K, 8>;
-  hipLaunchKernelGGL(f, dim3((unsigned)((c.E + SC_WAVES - 1) / SC_WAVES)), dim3(64 * SC_WAVES), alloc_scan_lds_bytes(c), st, d, io);
+  const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : 8;
+  const bool t = alloc_scan_tab(c, GW);
+  KFn f = GW == 2 ? (t ? (KFn)alloc_scan_kernel<K, 2, true> : (KFn)alloc_scan_kernel<K, 2, false>)
+        : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true> : (KFn)alloc_scan_kernel<K, 4, false>)
+                  : (t ? (KFn)alloc_scan_kernel<K, 8, true> : (KFn)alloc_scan_kernel<K, 8, false>);
+  const size_t lds = alloc_scan_lds_bytes(c);
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(f, dim3((unsigned)((c.E + SC_WAVES - 1) / SC_WAVES)), dim3(64 * SC_WAVES), lds, st, d, io);
 }
 
 hipError_t launch_alloc_scan(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
@@ -356,5 +465,16 @@ hipError_t launch_alloc_scan(const EnvConst& c, const DevEnv* d, const StepIO& i
   }
   return hipGetLastError();
 }
+
+#ifdef MSC_PROF
+extern "C" int msc_debug_prof_scan(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof_scan), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof_scan), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 }  // namespace msc

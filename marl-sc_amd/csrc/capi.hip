@@ -61,7 +61,7 @@ struct msc_env {
   int t_cap = 0, n_tdem = 0, n_tstep = 0;
   // Episode-ahead demand (EA; few envs per GPU). A Poisson episode's orders
   // depend only on its seed (SeedSequence([root, counter]), seed_manager.py:100-120), not on
-  // actions, so whole future episodes are generated on `ea_stream` while earlier ones step: slot
+  // actions, so whole future episodes are generated on side streams while earlier ones step: slot
   // n % S holds episode n (counted from the snapshot taken when EA started, episode 0 = the one
   // running then, which keeps the per-step path). At the end of episode n its slot is refilled
   // with episode n + S. Any desynchronising event (masked reset, load_state, disabling) stops it;
@@ -71,7 +71,11 @@ struct msc_env {
   int64_t ea_n = 0;         // episode (relative to the snapshot) the envs are in
   int ea_cur = -1;          // slot of the current episode, -1: per-step demand
   void* ea_mem = nullptr;
-  hipStream_t ea_stream = nullptr;
+  // One episode of E lanes is a chain of T per-step parses (~60 ms at 8 x 64 x 5 whatever the lane
+  // count) while the envs consume one in T steps: slot j is refilled on stream j % EA_STREAMS so that
+  // several episodes generate concurrently.
+  static constexpr int EA_STREAMS = 4;
+  hipStream_t ea_stream[EA_STREAMS] = {};
   hipEvent_t ev_gen[MSC_EA_MAX_S] = {}, ev_cons[MSC_EA_MAX_S] = {}, ev_snap = nullptr;
   std::vector<hipEvent_t> tev_ea;  // timing of EA launches (msc_env_set_timing)
   int n_tea = 0;
@@ -92,14 +96,30 @@ static hipError_t tmark(const msc_env* env, const std::vector<hipEvent_t>& v, in
 }
 
 // ---- episode-ahead demand (see msc_env) ----------------------------------------------------
+static hipStream_t ea_stream_of(const msc_env* env, int slot) { return env->ea_stream[slot % msc_env::EA_STREAMS]; }
+// every EA stream waits for `ev` (recorded on `st` first)
+static int ea_streams_wait(msc_env* env, hipStream_t st) {
+  HIP_TRY(hipEventRecord(env->ev_snap, st));
+  for (int i = 0; i < msc_env::EA_STREAMS; i++) HIP_TRY(hipStreamWaitEvent(env->ea_stream[i], env->ev_snap, 0));
+  return 0;
+}
+// `st` waits for every EA stream's work so far
+static int wait_ea_streams(msc_env* env, hipStream_t st) {
+  for (int i = 0; i < msc_env::EA_STREAMS; i++) {
+    HIP_TRY(hipEventRecord(env->ev_snap, env->ea_stream[i]));
+    HIP_TRY(hipStreamWaitEvent(st, env->ev_snap, 0));
+  }
+  return 0;
+}
 static hipError_t ea_launch(msc_env* env, int slot0, int nslots, int from_slot, int iters0) {
+  hipStream_t es = ea_stream_of(env, slot0);
   const bool tm = env->n_tea < env->t_cap;
-  if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea], env->ea_stream);
-  hipError_t e = launch_demand_ea(env->c, env->dev, EaLaunch{slot0, nslots, from_slot, iters0}, env->ea_stream);
+  if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea], es);
+  hipError_t e = launch_demand_ea(env->c, env->dev, EaLaunch{slot0, nslots, from_slot, iters0}, es);
   if (e != hipSuccess) return e;
-  if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea++ + 1], env->ea_stream);
+  if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea++ + 1], es);
   for (int k = 0; k < nslots; k++) {
-    e = hipEventRecord(env->ev_gen[(slot0 + k) % env->c.ea_S], env->ea_stream);
+    e = hipEventRecord(env->ev_gen[(slot0 + k) % env->c.ea_S], es);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -108,12 +128,11 @@ static hipError_t ea_launch(msc_env* env, int slot0, int nslots, int from_slot, 
 // the current episode -> slot 0's counter; episodes 1 .. S-1 are generated in one launch.
 static int ea_start(msc_env* env, hipStream_t st) {
   const int S = env->c.ea_S;
-  HIP_TRY(hipEventRecord(env->ev_snap, env->ea_stream));  // EA work of an earlier run still reads ea_cnt
-  HIP_TRY(hipStreamWaitEvent(st, env->ev_snap, 0));
+  if (const int rc = wait_ea_streams(env, st)) return rc;  // EA work of an earlier run still reads ea_cnt
   HIP_TRY(hipMemcpyAsync(env->s.ea_cnt, env->s.counter, sizeof(int32_t) * env->c.E, hipMemcpyDeviceToDevice, st));
-  HIP_TRY(hipEventRecord(env->ev_snap, st));
-  HIP_TRY(hipStreamWaitEvent(env->ea_stream, env->ev_snap, 0));
-  HIP_TRY(ea_launch(env, 1, S - 1, 0, 1));
+  if (const int rc = ea_streams_wait(env, st)) return rc;
+  // episodes 1 .. S-1: one launch per EA stream (slots 1 + i, 1 + i + EA_STREAMS, ... share none)
+  for (int k = 1; k < S; k++) HIP_TRY(ea_launch(env, k, 1, 0, k));
   env->ea_running = true;
   env->ea_n = 0;
   env->ea_cur = -1;
@@ -574,8 +593,9 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   }
   (void)hipEventRecord(env->ev_reset, env->side);
   if (env->ea_enabled) {
-    if (hipStreamCreateWithFlags(&env->ea_stream, hipStreamNonBlocking) != hipSuccess)
-      return fail(set_err(-2, "EA stream creation failed"));
+    for (int i = 0; i < msc_env::EA_STREAMS; i++)
+      if (hipStreamCreateWithFlags(&env->ea_stream[i], hipStreamNonBlocking) != hipSuccess)
+        return fail(set_err(-2, "EA stream creation failed"));
     for (int j = 0; j < MSC_EA_MAX_S; j++)
       if (hipEventCreateWithFlags(&env->ev_gen[j], hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&env->ev_cons[j], hipEventDisableTiming) != hipSuccess)
@@ -583,8 +603,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     if (hipEventCreateWithFlags(&env->ev_snap, hipEventDisableTiming) != hipSuccess)
       return fail(set_err(-2, "event creation failed"));
     for (int j = 0; j < MSC_EA_MAX_S; j++) {
-      (void)hipEventRecord(env->ev_gen[j], env->ea_stream);
-      (void)hipEventRecord(env->ev_cons[j], env->ea_stream);
+      (void)hipEventRecord(env->ev_gen[j], env->ea_stream[0]);
+      (void)hipEventRecord(env->ev_cons[j], env->ea_stream[0]);
     }
   }
   *out = env;
@@ -612,7 +632,8 @@ void msc_env_destroy(msc_env* env) {
   if (env->ea_mem) (void)hipFree(env->ea_mem);
   timing_free(env);
   if (env->side) (void)hipStreamDestroy(env->side);
-  if (env->ea_stream) (void)hipStreamDestroy(env->ea_stream);
+  for (int i = 0; i < msc_env::EA_STREAMS; i++)
+    if (env->ea_stream[i]) (void)hipStreamDestroy(env->ea_stream[i]);
   delete env;
 }
 
@@ -716,7 +737,7 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
     // has read it
     const int slot = (int)(env->ea_n % c.ea_S);
     HIP_TRY(hipEventRecord(env->ev_cons[slot], st));
-    HIP_TRY(hipStreamWaitEvent(env->ea_stream, env->ev_cons[slot], 0));
+    HIP_TRY(hipStreamWaitEvent(ea_stream_of(env, slot), env->ev_cons[slot], 0));
     HIP_TRY(ea_launch(env, slot, 1, slot, c.ea_S));
     env->ea_n++;
   }

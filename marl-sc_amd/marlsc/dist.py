@@ -42,11 +42,16 @@ def allreduce_adv_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     return stats
 
 
-def mean_std(stats: torch.Tensor) -> Tuple[float, float]:
-    """Global mean and (population) std from reduced [sum, sum_sq, n]."""
-    s, ss, n = (float(v) for v in stats.reshape(-1).tolist())
-    if n <= 0:
-        raise ValueError("no advantages")
-    mean = s / n
-    var = max(ss / n - mean * mean, 0.0)
-    return mean, math.sqrt(var)
+def mean_std(stats: torch.Tensor):
+    """Global mean and (population) std from reduced [sum, sum_sq, n]: floats for a [3] table,
+    lists of G floats each for a [G, 3] one (one row per module)."""
+    rows = stats.reshape(-1, 3).tolist()
+    out = []
+    for s, ss, n in rows:
+        if n <= 0:
+            raise ValueError("no advantages")
+        mean = s / n
+        out.append((mean, math.sqrt(max(ss / n - mean * mean, 0.0))))
+    if stats.dim() == 1:
+        return out[0]
+    return [m for m, _ in out], [sd for _, sd in out]

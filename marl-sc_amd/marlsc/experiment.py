@@ -8,17 +8,23 @@ evaluation and W&B are out of scope; their flags are accep
     python -m marlsc.experiment --mode evaluate --storage-dir ./experiment_outputs \
         --experiment-name NAME --eval-episodes 100 --root-seed 42
 
-Multi-GPU: launch `single` with torchrun (one process per GPU, RCCL); each rank owns
-`--envs` envs (global env ids), gradients and advantage statistics are all-reduced.
-Output layout (per experiment): config_env.yaml, config_algorithm.yaml, run_metadata.json,
-training_metrics.jsonl, checkpoints/checkpoint_NNNNNN/, checkpoints/checkpoint_final/,
-eval_results.json (evaluate mode).
+Multi-GPU: launch `single` with torchrun (one process per GPU, RCCL; MSC_DIST_BACKEND=gloo
+rehearses it on CPU-side collectives); each rank owns `--envs` envs (global env ids), gradients and
+advantage statistics are all-reduced.
+Output layout (per experiment directory, as the reference's ExperimentRunner writes it,
+src/experiments/runner.py:163-395): checkpoint_<N>/ every checkpoint_freq iterations,
+checkpoint_best/ on each new best train return, checkpoint_final/, module_weights.pt (the state
+dict of agent 0's policy module, src/utils/weight_transfer.py:15-33), training_metrics.yaml
+({iteration, train_return, eval_return} per iteration; truncated to N on --resume-from
+checkpoint_<N>, runner.py:231-288), metadata.json, config_env.yaml, config_algorithm.yaml; plus
+training_metrics.jsonl (every result key per iteration) and eval_results.json (evaluate mode).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import re
 import shutil
 import sys
 import time
@@ -54,14 +60,57 @@ def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
 
 
 def _dist_setup():
+    """One process per GPU (torchrun env). Backend: MSC_DIST_BACKEND (default nccl = RCCL on ROCm;
+    gloo rehearses the multi-rank path, e.g. several ranks sharing one GPU)."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("MSC_DIST_BACKEND", "nccl")
+        dev = local % max(1, torch.cuda.device_count()) if torch.cuda.is_available() else 0
+        if torch.cuda.is_available():
+            torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+        local = dev
     return (dist.get_rank() if world > 1 else 0), world, local
+
+
+# ---- run-directory bookkeeping of the reference runner (src/experiments/runner.py,
+# ---- src/experiments/utils/experiment_utils.py:256-467)
+_CKPT_RE = re.compile(r"^checkpoint_(\d+)$")
+
+
+def parse_checkpoint_iteration(path) -> Optional[int]:
+    """N of a checkpoint_<N> directory; None for checkpoint_best / checkpoint_final."""
+    m = _CKPT_RE.match(Path(path).name)
+    return int(m.group(1)) if m else None
+
+
+def save_training_metrics(out: Path, metrics: List[Dict[str, Any]]) -> None:
+    with open(out / "training_metrics.yaml", "w", encoding="utf-8") as f:
+        yaml.dump(metrics, f, default_flow_style=False, sort_keys=False)
+
+
+def load_and_truncate_training_metrics(out: Path, completed: int):
+    """training_metrics.yaml entries with iteration <= completed, and the best train return among
+    them (-inf / None when there is none)."""
+    metrics: List[Dict[str, Any]] = []
+    path = out / "training_metrics.yaml"
+    if path.exists():
+        existing = yaml.safe_load(path.read_text()) or []
+        if isinstance(existing, list):
+            metrics = [m for m in existing if isinstance(m, dict) and isinstance(m.get("iteration"), int)
+                       and m["iteration"] <= completed]
+    best, best_it = float("-inf"), None
+    for m in metrics:
+        tr = m.get("train_return")
+        if isinstance(tr, (int, float)) and tr > best:
+            best, best_it = float(tr), m["iteration"]
+    return metrics, best, best_it
 
 
 def _load_configs(env_path: str, algo_path: str):
@@ -86,38 +135,78 @@ def run_single(args) -> Dict[str, Any]:
     out = Path(args.storage_dir) / name
     trainer = PPOTrainer(env_cfg, cfg, root_seed=root_seed, n_envs=args.envs, rollout_len=args.rollout_len,
                          device=device, eval_seed=args.eval_seed)
+    metrics: List[Dict[str, Any]] = []
+    best, best_it = float("-inf"), None
     if args.resume_from:
+        # runner.py:231-288: resume from checkpoint_<N>, metrics truncated to N, best restored
+        completed = parse_checkpoint_iteration(args.resume_from)
+        if completed is None:
+            raise ValueError("--resume-from must point at a 'checkpoint_<N>' directory so training can continue "
+                             f"from iteration N+1. Got: {args.resume_from}")
         trainer.load_checkpoint(args.resume_from)
+        if trainer.iteration != completed:
+            raise ValueError(f"{args.resume_from} holds iteration {trainer.iteration}, not {completed}")
+        metrics, best, best_it = load_and_truncate_training_metrics(out, completed)
     if rank == 0:
-        (out / "checkpoints").mkdir(parents=True, exist_ok=True)
+        out.mkdir(parents=True, exist_ok=True)
         shutil.copyfile(args.env_config, out / "config_env.yaml")
         shutil.copyfile(args.algorithm_config, out / "config_algorithm.yaml")
-        (out / "run_metadata.json").write_text(json.dumps({
-            "root_seed": root_seed, "train_seed": trainer.train_seed, "eval_seed": trainer.eval_seed,
-            "n_gpus": world, "envs_per_gpu": trainer.E, "rollout_len": trainer.T, "algorithm": cfg.name}, indent=1))
-    metrics_path = out / "training_metrics.jsonl"
+        meta = out / "metadata.json"
+        if not meta.exists():  # written once per run (experiment_utils.save_run_metadata)
+            meta.write_text(json.dumps({
+                "root_seed": root_seed, "train_seed": trainer.train_seed, "eval_seed": trainer.eval_seed,
+                "n_gpus": world, "envs_per_gpu": trainer.E, "rollout_len": trainer.T, "algorithm": cfg.name}, indent=1))
+        if args.resume_from:  # the detailed log is truncated like the yaml one
+            jl = out / "training_metrics.jsonl"
+            if jl.exists():
+                keep = [ln for ln in jl.read_text().splitlines()
+                        if ln.strip() and json.loads(ln).get("training_iteration", 0) <= trainer.iteration]
+                jl.write_text("".join(k + "\n" for k in keep))
     last: Dict[str, Any] = {}
     while trainer.iteration < cfg.num_iterations:
         t0 = time.perf_counter()
         res = trainer.train_iteration()
-        if cfg.eval_interval and trainer.iteration % cfg.eval_interval == 0:
+        it = trainer.iteration
+        if cfg.eval_interval and it % cfg.eval_interval == 0:
             res.update(trainer.evaluate())
         res["time_this_iter_s"] = time.perf_counter() - t0
+        train_ret = res.get("train/episode_return_mean")
+        metrics.append({"iteration": it, "train_return": train_ret, "eval_return": res.get("eval/episode_return_mean")})
+        # checkpoint_best on a strictly better train return (runner.py:290-339); every rank saves its
+        # runtime state into the same directory, rank 0 the learner state
+        if train_ret is not None and train_ret > best:
+            best, best_it = float(train_ret), it
+            bp = out / "checkpoint_best"
+            if rank == 0 and bp.exists():
+                shutil.rmtree(bp)
+            _barrier(world)
+            trainer.save_checkpoint(bp)
         if rank == 0:
-            with open(metrics_path, "a") as f:
+            save_training_metrics(out, metrics)
+            with open(out / "training_metrics.jsonl", "a") as f:
                 f.write(json.dumps(res) + "\n")
-            ret = res.get("train/episode_return_mean")
-            print(f"[iter {trainer.iteration:4d}] env_steps={res['num_env_steps_sampled_lifetime']} "
-                  f"train_return={ret if ret is None else round(ret, 3)} "
+            print(f"[iter {it:4d}] env_steps={res['num_env_steps_sampled_lifetime']} "
+                  f"train_return={train_ret if train_ret is None else round(train_ret, 3)} "
                   f"eval_return={res.get('eval/episode_return_mean')} "
                   f"loss={res.get('learner/total_loss', float('nan')):.4f} ({res['time_this_iter_s']:.2f}s)",
                   flush=True)
-        # every rank writes its own runtime state (env blob, generators); rank 0 the learner state
-        if cfg.checkpoint_freq and trainer.iteration % cfg.checkpoint_freq == 0:
-            trainer.save_checkpoint(out / "checkpoints" / f"checkpoint_{trainer.iteration:06d}")
+        if cfg.checkpoint_freq and it % cfg.checkpoint_freq == 0:
+            trainer.save_checkpoint(out / f"checkpoint_{it}")
         last = res
-    trainer.save_checkpoint(out / "checkpoints" / "checkpoint_final")
+    if rank == 0 and best_it is not None:
+        print(f"[INFO] Best checkpoint: iteration {best_it} with reward: {best:.4f}")
+    trainer.save_checkpoint(out / "checkpoint_final")
+    if rank == 0:
+        trainer.export_module_weights(out / "module_weights.pt")
+        if metrics:
+            save_training_metrics(out, metrics)
     return last
+
+
+def _barrier(world: int) -> None:
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
 
 
 def run_evaluate(args) -> Dict[str, Any]:
@@ -125,9 +214,10 @@ def run_evaluate(args) -> Dict[str, Any]:
     if not args.experiment_name:
         raise SystemExit("--experiment-name is required for --mode evaluate")
     out = Path(args.storage_dir) / args.experiment_name
-    meta = json.loads((out / "run_metadata.json").read_text())
+    mp = out / "metadata.json"
+    meta = json.loads((mp if mp.exists() else out / "run_metadata.json").read_text())
     env_cfg, algo_raw, cfg = _load_configs(str(out / "config_env.yaml"), str(out / "config_algorithm.yaml"))
-    ckpt = Path(args.checkpoint) if args.checkpoint else out / "checkpoints" / "checkpoint_final"
+    ckpt = Path(args.checkpoint) if args.checkpoint else out / "checkpoint_final"
     state = json.loads((ckpt / "state.json").read_text())
     env_meta = {}
     if state.get("obs_stats") is not None:

@@ -361,6 +361,10 @@ class PPOLearner:
         out = {k: v / max(n, 1) for k, v in acc.items()}
         out["num_minibatch_steps"] = n
         if cfg.use_kl_loss:  # RLlib's adaptive KL coefficient, per module
+            if self.world > 1:  # the ranks' mean KL: every rank keeps the same coefficients
+                t = torch.tensor(kl_sum, dtype=torch.float64, device=obs.device)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                kl_sum = [float(x) / self.world for x in t.tolist()]
             for j in range(len(streams)):
                 kl = kl_sum[j] / max(n, 1)
                 if kl > 2.0 * cfg.kl_target:
@@ -607,9 +611,26 @@ class PPOTrainer:
                     "n_episodes": self._n_episodes}, p / f"runtime_rank{self.rank}.pt")
         return p
 
-    def load_checkpoint(self, path: Union[str, Path], runtime: bool = True) -> None:
-        """Restore the learner (and with runtime=True this rank's env / generator state: resume)."""
+    def export_module_weights(self, path: Union[str, Path]) -> Path:
+        """module_weights.pt: the state dict of the policy module agent 0 maps to (the shared policy,
+        or agent 0's own), keys actor.* / critic.* / log_std as the reference RLModule's
+        (src/utils/weight_transfer.py:15-33, runner.py:379-395)."""
         p = Path(path)
+        p.parent.mkdir(parents=True, exist_ok=True)
+        torch.save(self.module.policies[0].state_dict(), p)
+        return p
+
+    def load_checkpoint(self, path: Union[str, Path], runtime: bool = True) -> None:
+        """Restore the learner (and with runtime=True this rank's env / generator state: resume).
+        A runtime resume needs the saved world size: each rank's env shard and sampled timesteps
+        assume it."""
+        p = Path(path)
+        sj = p / "state.json"
+        if runtime and sj.exists():
+            saved_world = json.loads(sj.read_text()).get("world_size", self.world)
+            if int(saved_world) != self.world:
+                raise ValueError(f"{p} was saved by {saved_world} ranks, this run has {self.world}: resume with the "
+                                 f"same rank count, or load the weights only (runtime=False)")
         st = torch.load(p / "learner_state.pt", map_location=self.device, weights_only=True)
         self.module.load_state_dict(st["module"])
         self.learner.opt.load_state_dict(st["optimizer"])

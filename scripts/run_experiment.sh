@@ -6,6 +6,8 @@
 #
 # Override with environment variables:
 #   ENV_CONFIG ALGO_CONFIG STORAGE_DIR EXPERIMENT_NAME ROOT_SEED EVAL_EPISODES NGPUS EXTRA_ARGS
+# The algorithm YAMLs carry the reference's sampling setup (2 runners x 10 envs); on the GPU pass
+# the env count per GPU, e.g. EXTRA_ARGS="--envs 4096" (BASELINE configs[1]).
 set -euo pipefail
 cd "$(dirname "$0")/.."
 export PYTHONPATH="$(pwd)/marl-sc_amd${PYTHONPATH:+:$PYTHONPATH}"

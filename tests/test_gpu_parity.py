@@ -352,9 +352,11 @@ def test_pipelined_equals_sequential_across_resets_and_checkpoints():
     assert np.array_equal(sa["inventory"], sb["inventory"])
 
 
-def test_launch_timing_counts_and_results_unchanged():
+def test_launch_timing_counts_and_results_unchanged(monkeypatch):
     # msc_env_set_timing (bench.py's roofline durations) only adds events: same results, one
-    # demand + one step launch timed per step while enabled, nothing after max_steps
+    # demand + one step launch timed per step while enabled, nothing after max_steps (per-step
+    # demand; episode-ahead generation is timed per episode launch: test_episode_ahead_...)
+    monkeypatch.setenv("MSC_EA", "0")
     cfg = make_synthetic_env_config(4, 8, 3, episode_length=5)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     a, b = _vec(spec, 128, base_seed=3), _vec(spec, 128, base_seed=3)

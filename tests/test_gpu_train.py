@@ -96,11 +96,46 @@ def test_experiment_cli_single_then_evaluate(tmp_path):
     out = tmp_path / "T"
     lines = (out / "training_metrics.jsonl").read_text().strip().splitlines()
     assert len(lines) == 2 and json.loads(lines[-1])["training_iteration"] == 2
-    assert (out / "checkpoints" / "checkpoint_final" / "learner_state.pt").exists()
+    assert (out / "checkpoint_final" / "learner_state.pt").exists()
+    assert (out / "metadata.json").exists() and (out / "module_weights.pt").exists()
     assert main(["--mode", "evaluate", "--storage-dir", str(tmp_path), "--experiment-name", "T",
                  "--eval-episodes", "3", "--root-seed", "42"]) == 0
     res = json.loads((out / "eval_results.json").read_text())
     assert res["eval/episodes"] == 3 and res["iteration"] == 2
+
+
+def test_experiment_resume_truncates_metrics_and_exports_module_weights(tmp_path):
+    # the reference runner's run directory (runner.py:163-395): checkpoint_<N> every checkpoint_freq
+    # iterations, checkpoint_best on a new best train return, checkpoint_final, module_weights.pt
+    # (agent 0's policy module state dict), training_metrics.yaml; --resume-from checkpoint_<N>
+    # truncates the metrics to N and continues at N + 1
+    from marlsc.experiment import main
+    env = REPO / "config_files/environments/env_c1_2wh4r2sku.yaml"
+    raw = yaml.safe_load(open(REPO / "config_files/algorithms/mappo.yaml"))
+    raw["algorithm"]["shared"].update(checkpoint_freq=1, num_epochs=1, num_minibatches=2, eval_interval=0)
+    algo = tmp_path / "mappo_ck1.yaml"
+    algo.write_text(yaml.safe_dump(raw))
+    args = ["--mode", "single", "--env-config", str(env), "--algorithm-config", str(algo),
+            "--storage-dir", str(tmp_path), "--experiment-name", "R", "--root-seed", "42",
+            "--envs", "16", "--rollout-len", "60"]
+    assert main(args + ["--num-iterations", "3"]) == 0
+    out = tmp_path / "R"
+    for n in (1, 2, 3):
+        assert (out / f"checkpoint_{n}" / "learner_state.pt").exists()
+    assert (out / "checkpoint_best" / "learner_state.pt").exists()
+    met = yaml.safe_load((out / "training_metrics.yaml").read_text())
+    assert [m["iteration"] for m in met] == [1, 2, 3] and set(met[0]) == {"iteration", "train_return", "eval_return"}
+    # resume from checkpoint_2: the log restarts after entry 2 and runs to 4
+    assert main(args + ["--num-iterations", "4", "--resume-from", str(out / "checkpoint_2")]) == 0
+    met2 = yaml.safe_load((out / "training_metrics.yaml").read_text())
+    assert [m["iteration"] for m in met2] == [1, 2, 3, 4]
+    assert met2[:2] == met[:2]
+    w = torch.load(out / "module_weights.pt", weights_only=True)
+    keys = set(w)
+    assert {"log_std", "actor.0.weight", "actor.0.bias", "critic.0.weight"} <= keys
+    assert all(k.startswith(("actor.", "critic.")) or k == "log_std" for k in keys)
+    with pytest.raises(ValueError):  # only checkpoint_<N> carries the iteration to resume from
+        main(args + ["--num-iterations", "5", "--resume-from", str(out / "checkpoint_best")])
 
 
 def test_eval_envs_replay_the_reference_eval_episodes():

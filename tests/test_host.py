@@ -244,3 +244,112 @@ def test_synthetic_trace_packs_like_the_preprocessor_frame():
     assert p["n_rows"] == 20 and p["offsets"][-1] == n_orders
     assert int(p["quantities"].sum()) == int(tr["quantity"].sum())  # every line has a SKU in [0, 5)
     assert np.all(np.diff(p["regions"][p["offsets"][3]:p["offsets"][4]]) >= 0)  # region-major within a step
+
+
+def test_mean_std_per_module_rows():
+    import torch
+    sys.path.insert(0, str(REPO / "marl-sc_amd"))
+    from marlsc.dist import mean_std
+    rng = np.random.default_rng(1)
+    xs = [rng.normal(g, g + 1, 1000) for g in range(3)]
+    st = torch.tensor([[x.sum(), (x * x).sum(), x.size] for x in xs], dtype=torch.float64)
+    m, s = mean_std(st)
+    np.testing.assert_allclose(m, [x.mean() for x in xs], rtol=1e-12)
+    np.testing.assert_allclose(s, [x.std() for x in xs], rtol=1e-9)
+    m0, s0 = mean_std(st[1])
+    assert abs(m0 - xs[1].mean()) < 1e-12 and abs(s0 - xs[1].std()) < 1e-9
+
+
+def _learner_batch(S, W, L, K, seed):
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    return {"obs": torch.randn(S, W, L, generator=g), "actions": torch.randn(S, W, K, generator=g).clamp(-1, 1),
+            "logp": -torch.rand(S, W, generator=g) * 5, "advantages": torch.randn(S, W, generator=g),
+            "value_targets": torch.randn(S, W, generator=g),
+            "mean_old": torch.randn(S, W, K, generator=g) * 0.1, "log_std_old": torch.full((S, W, K), -1.4)}
+
+
+def _learner_cfg():
+    sys.path.insert(0, str(REPO / "marl-sc_amd"))
+    import yaml
+    from marlsc.ppo import PPOConfig
+    raw = yaml.safe_load(open(REPO / "config_files/algorithms/mappo.yaml"))
+    # one epoch, one minibatch = the whole (rank-local) batch: the update is then a function of the
+    # mean loss over every row, so the split over ranks must not change it
+    raw["algorithm"]["shared"].update(batch_size=64 * 3, num_epochs=1, num_minibatches=1)
+    return PPOConfig.from_algorithm_config(raw)
+
+
+def _learner_module(cfg, W, L, K):
+    import torch
+    from marlsc.ppo import MultiAgentActorCritic
+    torch.manual_seed(5)
+    return MultiAgentActorCritic(W, L, L * W, K, cfg.rollout_config(), cfg.parameter_sharing)
+
+
+def _learner_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from marlsc.ppo import PPOLearner, minibatch_rows
+    cfg = _learner_cfg()
+    W, L, K = 3, 7, 2
+    module = _learner_module(cfg, W, L, K)
+    batch = _learner_batch(64, W, L, K, seed=11)
+    mine = {k: v.chunk(world)[rank].contiguous() for k, v in batch.items()}  # this rank's envs
+    lr = PPOLearner(module, cfg, seed=rank)
+    assert lr.world == world and minibatch_rows(cfg, world) == 64 * 3 // world
+    stats = lr.update(mine)
+    assert stats["num_minibatch_steps"] == 1
+    torch.save(torch.tensor(lr.kl_coeffs, dtype=torch.float64), Path(out_dir) / f"kl{rank}.pt")
+    torch.save({k: v.detach() for k, v in module.state_dict().items()}, Path(out_dir) / f"p{rank}.pt")
+    dist.destroy_process_group()
+
+
+def test_learner_update_world2_gloo_equals_single_rank(tmp_path):
+    # 2 ranks x half the batch (gradients all-reduced, minibatch rows split by minibatch_rows(cfg,
+    # world)) against 1 rank x the whole batch: the same parameters after one PPOLearner.update
+    import socket
+    import torch
+    import torch.multiprocessing as mp
+    sys.path.insert(0, str(REPO / "marl-sc_amd"))
+    from marlsc.ppo import PPOLearner
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_learner_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    cfg = _learner_cfg()
+    W, L, K = 3, 7, 2
+    module = _learner_module(cfg, W, L, K)
+    p_init = {k: v.detach().clone() for k, v in module.state_dict().items()}
+    single = PPOLearner(module, cfg, seed=0)
+    single.update(_learner_batch(64, W, L, K, seed=11))
+    ref = module.state_dict()
+    for r in range(2):  # the adaptive KL coefficient follows the all-reduced mean KL
+        np.testing.assert_allclose(torch.load(tmp_path / f"kl{r}.pt").numpy(), single.kl_coeffs, rtol=1e-12)
+    p0 = torch.load(tmp_path / "p0.pt", weights_only=True)
+    p1 = torch.load(tmp_path / "p1.pt", weights_only=True)
+    moved = 0
+    for k in ref:
+        torch.testing.assert_close(p0[k], p1[k], rtol=0, atol=0)  # ranks stay identical
+        torch.testing.assert_close(p0[k], ref[k], rtol=1e-5, atol=2e-6)
+        moved += int(not torch.equal(ref[k], p_init[k]))
+    assert moved > 0
+
+
+def test_checkpoint_bookkeeping_of_the_reference_runner(tmp_path):
+    # experiment_utils.py:256-467: checkpoint_<N> names, training_metrics.yaml truncated to N on
+    # resume with the best train return re-derived from the surviving entries
+    sys.path.insert(0, str(REPO / "marl-sc_amd"))
+    from marlsc.experiment import load_and_truncate_training_metrics, parse_checkpoint_iteration, save_training_metrics
+    assert parse_checkpoint_iteration(tmp_path / "checkpoint_12") == 12
+    assert parse_checkpoint_iteration("runs/x/checkpoint_best") is None
+    assert parse_checkpoint_iteration("checkpoint_final") is None
+    assert parse_checkpoint_iteration("checkpoint_000003") == 3
+    m = [{"iteration": i, "train_return": r, "eval_return": None} for i, r in ((1, -5.0), (2, -3.0), (3, None), (4, -1.0))]
+    save_training_metrics(tmp_path, m)
+    kept, best, best_it = load_and_truncate_training_metrics(tmp_path, 3)
+    assert [x["iteration"] for x in kept] == [1, 2, 3] and best == -3.0 and best_it == 2
+    kept, best, best_it = load_and_truncate_training_metrics(tmp_path / "nowhere", 3)
+    assert kept == [] and best == float("-inf") and best_it is None

@@ -84,12 +84,18 @@ def test_packed_fragments_reproduce_the_mlp(L, H, KO, layout):
 
 
 def test_fusable_shapes():
-    assert fusable(list(MLP(34, 5, {"hidden_sizes": [256, 256]})))
-    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [256, 128]})))    # unequal hidden sizes
-    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [96, 96]})))      # not 64 / 128 / 256
+    from marlsc.mlp import fused_layers
+    assert fused_layers(list(MLP(34, 5, {"hidden_sizes": [256, 256]}))) == 3
+    assert fused_layers(list(MLP(34, 5, {"hidden_sizes": [256, 128]}))) == 3   # unequal two-layer sizes
+    assert fused_layers(list(MLP(34, 5, {"hidden_sizes": [512, 64]}))) == 3
+    assert fused_layers(list(MLP(34, 5, {"hidden_sizes": [256]}))) == 2        # the reference IPPO nets
+    assert fused_layers(list(MLP(306, 1, {"hidden_sizes": [1024]}))) == 2      # mappo_test critic
+    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [96, 96]})))      # two-layer: 64 / 128 / 256 / 512
+    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [1056]})))        # one layer: <= 1024
+    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [100]})))         # one layer: multiples of 32
     assert not fusable(list(MLP(34, 40, {"hidden_sizes": [64, 64]})))     # > 32 outputs
     assert not fusable(list(MLP(34, 5, {"hidden_sizes": [64, 64], "activation": "tanh"})))
-    assert not fusable(list(MLP(34, 5, {"hidden_sizes": [64]})))
+    assert not fusable(list(MLP(1100, 5, {"hidden_sizes": [64, 64]})))    # > 1024 inputs
 
 
 def test_mlp3_abi_rejects_bad_arguments_before_any_launch():
@@ -101,7 +107,7 @@ def test_mlp3_abi_rejects_bad_arguments_before_any_launch():
     p = C.c_void_p(16)  # never dereferenced: every call below fails validation first
     assert f(None, 8, 34, 256, 256, 5, p, p, p, p, p, p, p, None, 1, None) == -1
     assert b"null" in L.msc_last_error()
-    assert f(p, 8, 34, 256, 128, 5, p, p, p, p, p, p, p, None, 1, None) == -1
+    assert f(p, 8, 34, 256, 96, 5, p, p, p, p, p, p, p, None, 1, None) == -1
     assert b"hidden sizes" in L.msc_last_error()
     assert f(p, 8, 34, 96, 96, 5, p, p, p, p, p, p, p, None, 1, None) == -1
     assert f(p, 8, 34, 64, 64, 33, p, p, p, p, p, p, p, None, 1, None) == -1
@@ -111,6 +117,14 @@ def test_mlp3_abi_rejects_bad_arguments_before_any_launch():
     q = C.c_void_p(20)  # misaligned bias
     assert f(p, 8, 34, 64, 64, 5, p, q, p, p, p, p, p, None, 1, None) == -1
     assert b"aligned" in L.msc_last_error()
+    g = L.msc_mlp2_relu_forward  # the one-hidden-layer form
+    assert g(None, 8, 34, 256, 5, p, p, p, p, p, None, 1, None) == -1
+    assert b"null" in L.msc_last_error()
+    assert g(p, 8, 34, 100, 5, p, p, p, p, p, None, 1, None) == -1
+    assert b"hidden size" in L.msc_last_error()
+    assert g(p, 8, 34, 2048, 5, p, p, p, p, p, None, 1, None) == -1
+    assert g(p, 8, 2000, 256, 5, p, p, p, p, p, None, 1, None) == -1
+    assert b"in_dim" in L.msc_last_error()
 
 
 def test_output_layer_layout_rule():

@@ -28,10 +28,16 @@ def _cfg(name="mappo", **over):
 def test_algorithm_configs_parse_like_the_reference_schema():
     m = _cfg("mappo")
     assert m.name == "mappo" and m.critic_obs_type == "global" and m.parameter_sharing
-    assert m.num_minibatches == 8 and m.num_epochs == 10 and m.learning_rate == 5e-4
-    assert m.vf_clip_param == 10 and m.use_kl_loss is False  # schema defaults (schema.py:1102-1107)
+    # the reference's own config_files/algorithms/mappo.yaml / ippo.yaml values
+    assert m.num_minibatches == 10 and m.num_epochs == 20 and m.learning_rate == 0.0007598648793612028
+    assert m.vf_clip_param == 2046.8403482088547 and m.use_kl_loss is True and m.clip_param == 0.2
+    assert m.obs_normalization == "meanstd_custom" and m.logstd_floor == -3.51636237623627
+    assert m.networks["actor"]["config"]["hidden_sizes"] == [256, 256]
+    assert m.networks["critic"]["config"]["hidden_sizes"] == [64, 64]
     i = _cfg("ippo")
-    assert i.name == "ippo" and i.critic_obs_type == "local"
+    assert i.name == "ippo" and i.critic_obs_type == "local" and i.clip_param == 0.1 and i.use_kl_loss is False
+    assert i.networks["actor"]["config"]["hidden_sizes"] == [256] == i.networks["critic"]["config"]["hidden_sizes"]
+    assert i.obs_normalization == "meanstd_custom" and i.entropy_coeff == 0.004402763769660333
     from marlsc.ppo import PPOConfig
     with pytest.raises(ValueError):
         PPOConfig.from_algorithm_config({"algorithm": {"name": "cppo", "shared": {}, "algorithm_specific": {}}})
