@@ -288,11 +288,30 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
                         const float* eps, int64_t n_rows, int32_t k, float* actions, float* logp,
                         float* clipped, msc_stream_t stream);
 
+/* RLlib's MeanStdFilter env-to-module connector (obs_normalization "meanstd", the reference's
+ * src/algorithms/mappo.py:170-171 / ippo.py:173-175; evaluation applies it with update=False,
+ * base.py:131-140, :176-177), one RunningStat per column (agent x feature) of obs [n_rows][n_cols]:
+ *   update != 0: every row (in row order; only rows with mask[row] != 0 when mask is given) is
+ *   pushed (n += 1; M += (x - M) / n; S += (x - M_old)^2 (n - 1) / n) and normalised with the
+ *   statistics that include it; update == 0: normalised with the current statistics only.
+ *   out = clip((x - M) / (sqrt(var) + eps), -clip, clip) with var = S / (n - 1) (M^2 while n <= 1);
+ *   clip = 0 disables clipping. out may alias obs.
+ * state (device f64 [4 + 4 n_cols]): {n, buffer n, 0, 0, M[n_cols], S[n_cols], buffer M[n_cols],
+ * buffer S[n_cols]}; the buffer collects the pushes since the caller last cleared it (RLlib's filter
+ * buffer, merged across env runners by RunningStat.update). scratch: device f64
+ * [msc_meanstd_scratch_doubles(n_rows, n_cols)] (only with update). Rows are pushed sequentially
+ * within segments of ceil(n_rows / 64) rows and segment statistics combined by Chan's merge, so
+ * results match a sequential update to rounding (f64). */
+int64_t msc_meanstd_scratch_doubles(int64_t n_rows, int32_t n_cols);
+int msc_meanstd_filter(const float* obs, float* out, int64_t n_rows, int32_t n_cols, const uint8_t* mask,
+                       int32_t update, double* state, double* scratch, double clip, double eps,
+                       msc_stream_t stream);
+
 /* Rollout policy inference (replaces the actor's torch layer sequence in the EnvRunner's
  * _forward_inference, rlmodules/base.py:480-557, for MLPArchitecture.build networks,
  * architectures/mlp.py:14-60): out = W3 relu(W2 relu(W1 x + b1) + b2) + b3 for n_rows rows of
  * in_dim floats, in one kernel on the f32 MFMA (hidden activations stay in registers).
- * hidden1 == hidden2 in {64, 128, 256}; out_dim <= 32. Weights are passed in the packed fragment
+ * hidden1, hidden2 in {64, 128, 256, 512} (equal or not); out_dim <= 32. Weights are passed in the packed fragment
  * order the kernel streams (marlsc/mlp.py:pack_mlp3 builds them from the torch [out, in] matrices):
  *   w1p [hidden1/32][ceil(ceil(in_dim/2)/4)][64][4], w2p [hidden2/32][hidden1/8][64][4], and w3p either
  *   [hidden2/8][64][4] (MFMA output layer) or [hidden2/2][2][8] (VALU output layer, out_dim <= 8):
@@ -302,7 +321,6 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
  * the first layer's pre-activation of every row n as pre1[n / pre1_group]: the MAPPO critic's
  * first layer over local_w || global (multi_env.py:566-573) is W_local x_w + (W_global g_env + b1),
  * with the global block computed once per env (pre1_group = agents). */
-/* hidden1, hidden2 in {64, 128, 256, 512} (equal or not). */
 int msc_mlp3_w3_layout(int32_t out_dim);
 int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
                           int32_t out_dim, const float* w1p, const float* b1, const float* w2p, const float* b2,

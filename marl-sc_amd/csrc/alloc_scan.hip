@@ -85,6 +85,18 @@ __device__ __forceinline__ int group_scan(int x, int p) {
   }
   return v;
 }
+// OR of a value over the 64 / GW groups (lanes p, p + GW, p + 2 GW, ...): row rotations inside the
+// 16-lane rows, then the gfx950 row / half swaps across them
+template <int GW>
+__device__ __forceinline__ uint32_t or_groups(uint32_t v) {
+  if constexpr (GW <= 2) v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false);  // row_ror:2
+  if constexpr (GW <= 4) v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);                        // row_ror:8
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = a[0] | a[1];
+  const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return b[0] | b[1];
+}
 // OR of the 64 / GW groups' GW-bit fields of a ballot
 template <int GW>
 __device__ __forceinline__ uint32_t fold_groups(uint64_t b) {
@@ -119,10 +131,13 @@ __device__ __forceinline__ uint32_t rec_field(const uint4& v, int h) {  // h: co
 // Orders of one region with the same cost ranking form a batch: greedy fills of consecutive orders
 // over one ranking are the fills of their running demand total, so order k of a batch takes
 //     f_{k,p,s} = a_k - a_{k-1},  a_k = min(inv_{p,s}, max(0, D_{k,s} - sum_{q<p} inv_{q,s})),
-// D_k = d_1 + ... + d_k, and the whole batch needs one permute, one scan and one bpermute; per order
-// only the contributing-warehouse flags (shipment counts) and the lost-order test remain, a few
-// VALU instructions without any LDS round trip. (With max_splits limiting the warehouses per order
-// every order is its own batch.)
+// D_k = d_1 + ... + d_k, and the whole batch needs one permute, one scan and one bpermute. As D_k
+// only grows, the orders rank p fills from are the ones asking for s in the run
+//     D_k > excl_p  and  D_{k-1} < incl_p     (inventory > 0)
+// and the orders short of s (lost-order test) those asking for it with D_k > the SKU total: per
+// order three threshold counts of D_k, the order masks follow per batch (batches of <= 16 orders;
+// contribution and lost masks in one word OR-reduced over the SKU groups). (With max_splits
+// limiting the warehouses per order every order is its own batch, with per-order ballots.)
 template <int K, int GW, bool TAB>
 __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   static_assert(K * GW <= 64 && K <= 6, "lane = s * GW + w; one uint4 per order record");
@@ -318,8 +333,16 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       rho_prev = cur_rho;
     }
     const bool inw = lane < nw;
+    const uint64_t inwm = __ballot(inw);
     const uint64_t rstart = __ballot(inw && rg != rg_prev);
-    const uint64_t bstart = split ? __ballot(inw) : __ballot(inw && (rg != rg_prev || rho != rho_prev));
+    const uint64_t bstart = split ? inwm
+                                  : (__ballot(inw && (rg != rg_prev || rho != rho_prev)) | (inwm & 0x0001000100010000ull));
+    uint64_t nzl = 0;  // the window's orders asking for this lane's SKU
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const uint64_t b = __ballot(inw && rec_field(rv, 1 + j) != 0u);
+      nzl = sk == j ? b : nzl;
+    }
     Lw->rec[lane] = rv;
     wave_sync();
     SPROF_ADD(p_rank, SPROF_NOW() - t_r0);
@@ -347,15 +370,36 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       const int incl = group_scan<GW>(x, w);
       const int excl = incl - x;
       int D = 0, a_prev = 0, cnt_r = 0;
-      for (int k = i0; k < i1; k++) {
+      if (!split) {
+        int c1 = 0, c2 = 0, c3 = 0;  // orders with D <= excl, D < incl, D <= incl
+        for (int k = i0; k < i1; k++) {
+          const int d = dn;
+          dn = Lh[(k + 1) * 8 + fi];  // (k + 1 == 64: the scratch after the window, unused)
+          D += d;
+          c1 += D <= excl ? 1 : 0;
+          c2 += D < incl ? 1 : 0;
+          c3 += D <= incl ? 1 : 0;
+        }
+        const int L = i1 - i0;  // <= 16
+        const uint32_t nzb = (uint32_t)(nzl >> i0) & ((1u << L) - 1u);
+        const int hi = c2 < L - 1 ? c2 : L - 1;  // fills from orders c1 .. hi (relative to i0)
+        const uint32_t cm = (x > 0 && hi >= c1) ? nzb & ((2u << hi) - 1u) & ~((1u << c1) - 1u) : 0u;
+        const uint32_t lm = lastp ? nzb & ~((1u << c3) - 1u) : 0u;
+        const uint32_t both = or_groups<GW>(cm | (lm << 16));
+        cnt_r = __builtin_popcount(both & 0xFFFFu);
+        lost_cnt += __builtin_popcount((uint32_t)__builtin_amdgcn_readlane((int)both, GW - 1) >> 16);
+        const int need = D - excl;
+        a_prev = need > 0 ? (need < x ? need : x) : 0;
+        dsum += D;
+      } else for (int k = i0; k < i1; k++) {
         const int d = dn;
         if (k + 1 < i1) dn = Lh[(k + 1) * 8 + fi];
         D += d;
         const int need = D - excl;  // demand left after the cheaper ranks
-        const int a = need > 0 ? (need < x ? need : x) : 0;  // min(inv, max(0, D - prefix)): one v_med3
+        const int a = need > 0 ? (need < x ? need : x) : 0;  // min(inv, max(0, D - prefix))
         int f = a - a_prev;
         a_prev = a;
-        if (split) {  // max_splits: only the first max_wh contributing ranks ship (a one-order batch)
+        {  // max_splits: only the first max_wh contributing ranks ship (a one-order batch)
           uint32_t m = fold_groups<GW>(__ballot(f > 0));
           if (__builtin_popcount(m) > maxwh) {
             uint32_t keep = 0u;
@@ -371,10 +415,6 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
           const int rem = d - group_scan<GW>(f, w);  // (this SKU's total in its last rank lane)
           u += rem;
           lost_cnt += __ballot(lastp && rem > 0) != 0 ? 1 : 0;
-        } else {
-          cnt_r += (int)((fold_groups<GW>(__ballot(f > 0)) >> w) & 1u);
-          // the order is short of SKU s <=> it asks for s and the running demand exceeds the stock
-          lost_cnt += __ballot(lastp && d > 0 && D > incl) != 0 ? 1 : 0;
         }
         dsum += d;
       }

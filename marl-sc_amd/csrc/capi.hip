@@ -71,11 +71,22 @@ struct msc_env {
   int64_t ea_n = 0;         // episode (relative to the snapshot) the envs are in
   int ea_cur = -1;          // slot of the current episode, -1: per-step demand
   void* ea_mem = nullptr;
-  // One episode of E lanes is a chain of T per-step parses (~60 ms at 8 x 64 x 5 whatever the lane
-  // count) while the envs consume one in T steps: slot j is refilled on stream j % EA_STREAMS so that
-  // several episodes generate concurrently.
-  static constexpr int EA_STREAMS = 4;
-  hipStream_t ea_stream[EA_STREAMS] = {};
+  // One launch is a chain of T per-step parses (~60 ms at 8 x 64 x 5) whatever its lane count,
+  // while the envs consume an episode in T steps: freed slots are refilled ea_batch at a time, in
+  // one launch of ea_batch x E lanes on one stream (separate streams would share the process's few
+  // hardware queues and serialise anyway).
+  hipStream_t ea_stream = nullptr;
+  int ea_batch = 1;         // slots per refill launch
+  int ea_freed = 0;         // consumed slots not yet refilled
+  // A generation runs as chunks of ea_chunk steps, each launched once the previous one has finished
+  // (polled at every step call; flushed when a step needs the slot), so that the EA work queued on
+  // the device at any time -- what a device-wide synchronize waits for -- is one short chunk.
+  int ea_chunk = 10;
+  struct EaItem { EaLaunch l; int wait_cons; };  // wait_cons: slot whose ev_cons precedes chunk 0 (-1: none)
+  std::vector<EaItem> ea_q;  // generations not yet fully launched (head: the one in progress)
+  bool ea_chunk_out = false; // a chunk of the head item is in flight (ev_chunk)
+  hipEvent_t ev_chunk = nullptr;
+  bool gen_pending[MSC_EA_MAX_S] = {};  // slot's generation not fully launched (ev_gen stale)
   hipEvent_t ev_gen[MSC_EA_MAX_S] = {}, ev_cons[MSC_EA_MAX_S] = {}, ev_snap = nullptr;
   std::vector<hipEvent_t> tev_ea;  // timing of EA launches (msc_env_set_timing)
   int n_tea = 0;
@@ -96,43 +107,91 @@ static hipError_t tmark(const msc_env* env, const std::vector<hipEvent_t>& v, in
 }
 
 // ---- episode-ahead demand (see msc_env) ----------------------------------------------------
-static hipStream_t ea_stream_of(const msc_env* env, int slot) { return env->ea_stream[slot % msc_env::EA_STREAMS]; }
-// every EA stream waits for `ev` (recorded on `st` first)
-static int ea_streams_wait(msc_env* env, hipStream_t st) {
+// the EA stream waits for the work queued on `st` so far
+static int ea_stream_wait(msc_env* env, hipStream_t st) {
   HIP_TRY(hipEventRecord(env->ev_snap, st));
-  for (int i = 0; i < msc_env::EA_STREAMS; i++) HIP_TRY(hipStreamWaitEvent(env->ea_stream[i], env->ev_snap, 0));
+  HIP_TRY(hipStreamWaitEvent(env->ea_stream, env->ev_snap, 0));
   return 0;
 }
-// `st` waits for every EA stream's work so far
-static int wait_ea_streams(msc_env* env, hipStream_t st) {
-  for (int i = 0; i < msc_env::EA_STREAMS; i++) {
-    HIP_TRY(hipEventRecord(env->ev_snap, env->ea_stream[i]));
-    HIP_TRY(hipStreamWaitEvent(st, env->ev_snap, 0));
-  }
+// `st` waits for the EA stream's work so far
+static int wait_ea_stream(msc_env* env, hipStream_t st) {
+  HIP_TRY(hipEventRecord(env->ev_snap, env->ea_stream));
+  HIP_TRY(hipStreamWaitEvent(st, env->ev_snap, 0));
   return 0;
 }
-static hipError_t ea_launch(msc_env* env, int slot0, int nslots, int from_slot, int iters0) {
-  hipStream_t es = ea_stream_of(env, slot0);
+// one chunk [l.t0, l.t1) of a generation on the EA stream; after the last chunk the slots' ev_gen
+static hipError_t ea_launch_chunk(msc_env* env, const EaLaunch& l) {
+  hipStream_t es = env->ea_stream;
   const bool tm = env->n_tea < env->t_cap;
   if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea], es);
-  hipError_t e = launch_demand_ea(env->c, env->dev, EaLaunch{slot0, nslots, from_slot, iters0}, es);
+  hipError_t e = launch_demand_ea(env->c, env->dev, l, es);
   if (e != hipSuccess) return e;
   if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea++ + 1], es);
-  for (int k = 0; k < nslots; k++) {
-    e = hipEventRecord(env->ev_gen[(slot0 + k) % env->c.ea_S], es);
+  if (l.t1 >= env->c.T) {
+    for (int k = 0; k < l.nslots; k++) {
+      const int slot = (l.slot0 + k) % env->c.ea_S;
+      e = hipEventRecord(env->ev_gen[slot], es);
+      if (e != hipSuccess) return e;
+      env->gen_pending[slot] = false;
+    }
+  }
+  return hipEventRecord(env->ev_chunk, es);
+}
+// launch the next chunk of the head generation if none is in flight (block: even if one is)
+static hipError_t ea_pump(msc_env* env, bool block) {
+  if (env->ea_q.empty()) return hipSuccess;
+  if (env->ea_chunk_out && !block) {
+    const hipError_t q = hipEventQuery(env->ev_chunk);
+    if (q == hipErrorNotReady) return hipSuccess;
+    if (q != hipSuccess) return q;
+  }
+  msc_env::EaItem& it = env->ea_q.front();
+  EaLaunch& l = it.l;
+  if (it.wait_cons >= 0) {  // a refill: after the step that read the slots' previous episodes
+    const hipError_t w = hipStreamWaitEvent(env->ea_stream, env->ev_cons[it.wait_cons], 0);
+    if (w != hipSuccess) return w;
+    it.wait_cons = -1;
+  }
+  EaLaunch cl = l;
+  cl.t1 = l.t0 + env->ea_chunk < env->c.T ? l.t0 + env->ea_chunk : env->c.T;
+  const hipError_t e = ea_launch_chunk(env, cl);
+  if (e != hipSuccess) return e;
+  env->ea_chunk_out = true;
+  l.t0 = cl.t1;
+  if (l.t0 >= env->c.T) env->ea_q.erase(env->ea_q.begin());
+  return hipSuccess;
+}
+// queue a generation (slots slot0 .. slot0 + nslots - 1, see EaLaunch)
+static hipError_t ea_enqueue(msc_env* env, int slot0, int nslots, int from_slot, int iters0, int iters_step,
+                             int wait_cons = -1) {
+  env->ea_q.push_back({EaLaunch{slot0, nslots, from_slot, iters0, iters_step, 0, env->c.T}, wait_cons});
+  for (int k = 0; k < nslots; k++) env->gen_pending[(slot0 + k) % env->c.ea_S] = true;
+  return ea_pump(env, false);
+}
+// every chunk up to the generation of `slot` launched (its ev_gen is then current)
+static hipError_t ea_flush_to(msc_env* env, int slot) {
+  while (env->gen_pending[slot]) {
+    if (env->ea_q.empty()) return hipErrorInvalidValue;  // (unreachable: pending slots are queued)
+    const hipError_t e = ea_pump(env, true);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
 // Snapshot at a common episode start (t_sync == 0, after the reset): the SeedManager counter of
-// the current episode -> slot 0's counter; episodes 1 .. S-1 are generated in one launch.
+// the current episode -> slot 0's counter; episodes 1 .. S-1 follow from it, 1 .. B first (the
+// envs need episode 1 when the per-step episode 0 ends), then B+1 .. S-1.
 static int ea_start(msc_env* env, hipStream_t st) {
-  const int S = env->c.ea_S;
-  if (const int rc = wait_ea_streams(env, st)) return rc;  // EA work of an earlier run still reads ea_cnt
+  const int S = env->c.ea_S, B = env->ea_batch;
+  if (const int rc = wait_ea_stream(env, st)) return rc;  // EA work of an earlier run still reads ea_cnt
   HIP_TRY(hipMemcpyAsync(env->s.ea_cnt, env->s.counter, sizeof(int32_t) * env->c.E, hipMemcpyDeviceToDevice, st));
-  if (const int rc = ea_streams_wait(env, st)) return rc;
-  // episodes 1 .. S-1: one launch per EA stream (slots 1 + i, 1 + i + EA_STREAMS, ... share none)
-  for (int k = 1; k < S; k++) HIP_TRY(ea_launch(env, k, 1, 0, k));
+  if (const int rc = ea_stream_wait(env, st)) return rc;
+  const int first = B < S - 1 ? B : S - 1;
+  env->ea_q.clear();
+  env->ea_chunk_out = false;
+  for (int j = 0; j < S; j++) env->gen_pending[j] = false;
+  HIP_TRY(ea_enqueue(env, 1, first, 0, 1, 1));
+  if (first < S - 1) HIP_TRY(ea_enqueue(env, 1 + first, S - 1 - first, 0, 1 + first, 1));
+  env->ea_freed = 0;
   env->ea_running = true;
   env->ea_n = 0;
   env->ea_cur = -1;
@@ -153,6 +212,8 @@ static int ea_stop(msc_env* env, hipStream_t st, bool materialize) {
   }
   env->ea_running = false;
   env->ea_cur = -1;
+  env->ea_q.clear();  // generations not launched yet are dropped (chunks in flight finish on the EA stream)
+  for (int j = 0; j < MSC_EA_MAX_S; j++) env->gen_pending[j] = false;
   return 0;
 }
 
@@ -374,7 +435,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     if (d->demand_type == MSC_DEMAND_POISSON) {
       bool want = n_envs <= 8192;
       if (const char* ea = getenv("MSC_EA")) want = atoi(ea) != 0;
-      int S = 8;
+      int S = 12;
       if (const char* es = getenv("MSC_EA_SLOTS")) S = atoi(es);
       S = S < 2 ? 2 : (S > MSC_EA_MAX_S ? MSC_EA_MAX_S : S);
       if (want) {
@@ -542,6 +603,18 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       s.ea_pos = s2.ea_pos = (uint32_t*)(b + al(rec) + al(offb));
       s.ea_cnt = s2.ea_cnt = (int32_t*)(b + al(rec) + al(offb) + al(posb));
       env->ea_enabled = true;
+      // refill batch: a batch freed by episodes n-B+1 .. n is needed S-B episodes later
+      int B = S / 3 > 1 ? S / 3 : 1;
+      if (const char* eb = getenv("MSC_EA_BATCH")) B = atoi(eb);
+      env->ea_batch = B < 1 ? 1 : (B > S - 1 ? S - 1 : B);
+      // step_c's observation staging (up to 80 KB of LDS per block) stalls behind a generation
+      // chunk's pending blocks for the chunk's whole run (measured: 5.5 ms step_c launches right
+      // after a chunk starts, none without staging): off with EA unless MSC_OBS_STAGE=1
+      const char* os = getenv("MSC_OBS_STAGE");
+      if (!(os && atoi(os) != 0)) c.obs_stage = 0;
+      int ch = 10;
+      if (const char* ec = getenv("MSC_EA_CHUNK")) ch = atoi(ec);
+      env->ea_chunk = ch < 1 ? 1 : ch;
     } else {
       (void)hipGetLastError();
       env->ea_mem = nullptr;
@@ -593,18 +666,18 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   }
   (void)hipEventRecord(env->ev_reset, env->side);
   if (env->ea_enabled) {
-    for (int i = 0; i < msc_env::EA_STREAMS; i++)
-      if (hipStreamCreateWithFlags(&env->ea_stream[i], hipStreamNonBlocking) != hipSuccess)
-        return fail(set_err(-2, "EA stream creation failed"));
+    if (hipStreamCreateWithFlags(&env->ea_stream, hipStreamNonBlocking) != hipSuccess)
+      return fail(set_err(-2, "EA stream creation failed"));
     for (int j = 0; j < MSC_EA_MAX_S; j++)
       if (hipEventCreateWithFlags(&env->ev_gen[j], hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&env->ev_cons[j], hipEventDisableTiming) != hipSuccess)
         return fail(set_err(-2, "event creation failed"));
-    if (hipEventCreateWithFlags(&env->ev_snap, hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&env->ev_snap, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&env->ev_chunk, hipEventDisableTiming) != hipSuccess)
       return fail(set_err(-2, "event creation failed"));
     for (int j = 0; j < MSC_EA_MAX_S; j++) {
-      (void)hipEventRecord(env->ev_gen[j], env->ea_stream[0]);
-      (void)hipEventRecord(env->ev_cons[j], env->ea_stream[0]);
+      (void)hipEventRecord(env->ev_gen[j], env->ea_stream);
+      (void)hipEventRecord(env->ev_cons[j], env->ea_stream);
     }
   }
   *out = env;
@@ -629,11 +702,11 @@ void msc_env_destroy(msc_env* env) {
     if (env->ev_cons[j]) (void)hipEventDestroy(env->ev_cons[j]);
   }
   if (env->ev_snap) (void)hipEventDestroy(env->ev_snap);
+  if (env->ev_chunk) (void)hipEventDestroy(env->ev_chunk);
   if (env->ea_mem) (void)hipFree(env->ea_mem);
   timing_free(env);
   if (env->side) (void)hipStreamDestroy(env->side);
-  for (int i = 0; i < msc_env::EA_STREAMS; i++)
-    if (env->ea_stream[i]) (void)hipStreamDestroy(env->ea_stream[i]);
+  if (env->ea_stream) (void)hipStreamDestroy(env->ea_stream);
   delete env;
 }
 
@@ -709,9 +782,13 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
   // episode-ahead demand: start at a common episode start; an episode n >= 1 reads its slot
   if (env->ea_enabled && env->pipeline && !env->ea_running && env->t_sync == 0)
     if (const int rc = ea_start(env, st)) return rc;
+  if (env->ea_running) HIP_TRY(ea_pump(env, false));
   if (env->ea_running && env->t_sync == 0) {
     env->ea_cur = env->ea_n >= 1 ? (int)(env->ea_n % c.ea_S) : -1;
-    if (env->ea_cur >= 0) HIP_TRY(hipStreamWaitEvent(st, env->ev_gen[env->ea_cur], 0));
+    if (env->ea_cur >= 0) {
+      HIP_TRY(ea_flush_to(env, env->ea_cur));
+      HIP_TRY(hipStreamWaitEvent(st, env->ev_gen[env->ea_cur], 0));
+    }
   }
   io.ea_slot = env->ea_running ? env->ea_cur : -1;
   io.ea_t = env->t_sync;
@@ -733,12 +810,15 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
   env->ready[b] = false;
   const bool boundary = env->t_sync < 0 || env->t_sync + 1 >= c.T;
   if (env->ea_running && env->t_sync + 1 >= c.T) {
-    // episode ea_n ends with this step: its slot is refilled with episode ea_n + S once the step
-    // has read it
+    // episode ea_n ends with this step: its slot is to be refilled with episode ea_n + S once the
+    // step has read it; every ea_batch freed slots (consecutive mod S) go in one launch
     const int slot = (int)(env->ea_n % c.ea_S);
     HIP_TRY(hipEventRecord(env->ev_cons[slot], st));
-    HIP_TRY(hipStreamWaitEvent(ea_stream_of(env, slot), env->ev_cons[slot], 0));
-    HIP_TRY(ea_launch(env, slot, 1, slot, c.ea_S));
+    if (++env->ea_freed == env->ea_batch) {
+      const int B = env->ea_batch;
+      HIP_TRY(ea_enqueue(env, (slot - B + 1 + c.ea_S) % c.ea_S, B, -1, c.ea_S, 0, slot));
+      env->ea_freed = 0;
+    }
     env->ea_n++;
   }
   if (env->pipeline && !boundary && !ea_step) {
@@ -986,6 +1066,21 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
     return set_err(-1, "bad shape (n_rows %lld, k %d, log_std_rows %d)", (long long)n_rows, k, log_std_rows);
   HIP_TRY(launch_gauss_sample(mean, log_std, log_std_rows, logstd_floor, eps, n_rows, k, actions, logp, clipped,
                               (hipStream_t)stream));
+  return 0;
+}
+
+int64_t msc_meanstd_scratch_doubles(int64_t n_rows, int32_t n_cols) {
+  return n_rows >= 1 && n_cols >= 1 ? meanstd_scratch_doubles(n_rows, n_cols) : -1;
+}
+
+int msc_meanstd_filter(const float* obs, float* out, int64_t n_rows, int32_t n_cols, const uint8_t* mask,
+                       int32_t update, double* state, double* scratch, double clip, double eps,
+                       msc_stream_t stream) {
+  if (!obs || !out || !state || (update && !scratch)) return set_err(-1, "null argument");
+  if (n_rows < 1 || n_cols < 1) return set_err(-1, "bad shape (n_rows %lld, n_cols %d)", (long long)n_rows, n_cols);
+  if (!(eps >= 0.0) || !(clip >= 0.0)) return set_err(-1, "eps and clip must be >= 0");
+  HIP_TRY(launch_meanstd_filter(obs, out, n_rows, n_cols, mask, update ? 1 : 0, state, scratch, clip, eps,
+                                (hipStream_t)stream));
   return 0;
 }
 

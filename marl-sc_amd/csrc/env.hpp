@@ -109,9 +109,11 @@ struct EnvState {
 
 // one launch of the episode-ahead demand generator: lanes (k, e) for k < nslots generate the
 // episode of slot (slot0 + k) % S; its SeedManager counter follows from the counter stored for
-// from_slot by iters0 + k more resets (reset_env's eval cycling included)
+// from_slot (the lane's own slot when from_slot < 0) by iters0 + k * iters_step more resets
+// (reset_env's eval cycling included). A launch parses steps [t0, t1) of those episodes: t0 > 0
+// continues from the stream position / record count the launch of [.., t0) left in the slot.
 struct EaLaunch {
-  int32_t slot0, nslots, from_slot, iters0;
+  int32_t slot0, nslots, from_slot, iters0, iters_step, t0, t1;
 };
 
 // where an env's orders of this step are: record n, word v at base + n * nstep + v * vstep (uint4)
@@ -208,6 +210,9 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
 hipError_t launch_mlp2_relu(const float* x, int64_t n, int L, int H1, int KO, const float* w1p, const float* b1,
                             const float* w3p, const float* b3, float* out, const float* pre1, int grp, hipStream_t st);
 bool mlp2_supported(int H1);
+hipError_t launch_meanstd_filter(const float* x, float* out, int64_t E, int32_t C, const uint8_t* mask, int32_t update,
+                                 double* state, double* scratch, double clip, double eps, hipStream_t st);
+int64_t meanstd_scratch_doubles(int64_t E, int32_t C);
 hipError_t launch_gauss_sample(const float* mean, const float* log_std, int32_t ls_rows, float floor_, const float* eps,
                                int64_t N, int32_t K, float* act, float* logp, float* clipped, hipStream_t st);
 

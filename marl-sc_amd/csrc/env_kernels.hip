@@ -622,12 +622,13 @@ __device__ __forceinline__ int unit_quota(int tgt, int rdp) {
   return q < cap ? q : cap;
 }
 
-// EA: the root seed of the episode a lane generates (reset_env's counter rule applied iters0 + k
-// times from the counter stored for from_slot); the counter after that reset goes to cnt_out
+// EA: the root seed of the episode a lane generates (reset_env's counter rule applied
+// iters0 + k * iters_step times from the counter stored for from_slot, or for the lane's own slot
+// when from_slot < 0); the counter after that reset goes to cnt_out
 __device__ __forceinline__ uint32_t ea_root(const EnvConst& c, const EnvState& s, const EaLaunch& ea, int64_t e,
-                                            int k, int& cnt_out) {
-  int cnt = s.ea_cnt[(int64_t)ea.from_slot * c.E + e];
-  const int iters = ea.iters0 + k;
+                                            int k, int slot, int& cnt_out) {
+  int cnt = s.ea_cnt[(int64_t)(ea.from_slot < 0 ? slot : ea.from_slot) * c.E + e];
+  const int iters = ea.iters0 + k * ea.iters_step;
   int wv = 0;
   for (int i = 0; i < iters; i++) {
     wv = (c.num_eval > 0 && cnt >= c.num_eval) ? 0 : cnt;
@@ -701,11 +702,27 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   }
   double* myring = ring + lane;
   int ea_cnt_new = 0;
+  // EA chunk [t0, t1): stream position and record count where step t0 starts (0 for t0 == 0)
+  uint32_t ea_p0 = 0;
+  int ea_n0 = 0;
+  if constexpr (EA) {
+    if (valid && ea.t0 > 0) {
+      ea_p0 = s.ea_pos[((int64_t)slot * c.T + (ea.t0 - 1)) * E + e];
+      ea_n0 = s.ea_off[((int64_t)slot * (c.T + 1) + ea.t0) * E + e];
+    }
+  }
   auto start_rng = [&]() -> Pcg64 {
     if constexpr (EA) {
-      uint32_t root = ea_root(c, s, ea, e, ea_k, ea_cnt_new);
+      uint32_t root;
+      if (ea.t0 == 0) {
+        root = ea_root(c, s, ea, e, ea_k, slot, ea_cnt_new);
+      } else {  // the episode's counter is in the slot since its first chunk (wv = counter - 1)
+        const uint32_t w2[2] = {s.orig_root[e], (uint32_t)(s.ea_cnt[(int64_t)slot * E + e] - 1)};
+        root = ss_u32(w2, 2);
+      }
       Pcg64 r;
       pcg_seed_child(r, root, 2);  // 'demand_sampler' child of the episode's root (seed_manager.py:100-120)
+      if (ea_p0) pcg_advance(r, (uint64_t)ea_p0);
       return r;
     } else {
       return load_rng(s, 0, e, E);
@@ -773,8 +790,8 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   }
   rdv[lane] = 0;
   static_assert(K <= UD, "a mask unit completes in one round");
-  int st = valid ? PS_ORD : PS_DONE, r = 0, x = 0, left = 0, sq = 0, n = 0, rd = 0;
-  int tstep = 0;  // EA: step of the episode being parsed
+  int st = valid ? PS_ORD : PS_DONE, r = 0, x = 0, left = 0, sq = 0, n = ea_n0, rd = 0;
+  int tstep = EA ? ea.t0 : 0;  // EA: step of the episode being parsed
   unsigned mask = 0;
   int mf = 0, live = valid ? 1 : 0, pend = 0;
   const int cap = EA ? (int)c.ea_cap : c.order_cap;
@@ -784,15 +801,15 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   const int64_t vstride = EA ? 16 : E * 16;       // bytes between the uint4 words of a record
   const int64_t rstride = (int64_t)NV * vstride;  // bytes between consecutive records of a lane
   MSC_GLOBAL char* recp = reinterpret_cast<MSC_GLOBAL char*>(
-      gp(EA ? s.ea_rec + ((int64_t)slot * E + e) * c.ea_cap * NV : s.orders + e)) - rstride;
+      gp(EA ? s.ea_rec + ((int64_t)slot * E + e) * c.ea_cap * NV : s.orders + e)) + (int64_t)(n - 1) * rstride;
   // EA step boundaries: record offset / stream position after each step of the episode
   decltype(s.ea_off) ea_offp = EA ? s.ea_off + (int64_t)slot * (c.T + 1) * E + e : nullptr;
   decltype(s.ea_pos) ea_posp = EA ? s.ea_pos + (int64_t)slot * c.T * E + e : nullptr;
-  const int T_s = __builtin_amdgcn_readfirstlane(c.T);
+  const int T_s = __builtin_amdgcn_readfirstlane(EA ? ea.t1 : c.T);  // EA: the chunk's last step + 1
   __syncthreads();
   if constexpr (EA) {
     // (after the barrier: every wave of the block has read the slot's previous counter)
-    if (valid) {
+    if (valid && ea.t0 == 0) {
       s.ea_cnt[(int64_t)slot * E + e] = ea_cnt_new;
       ea_offp[0] = 0;
     }
@@ -827,7 +844,7 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     if constexpr (EA) {
       if (new_region & (r + 1 == R_s ? 1 : 0)) {
         ea_offp[(int64_t)(tstep + 1) * E] = n;
-        ea_posp[(int64_t)tstep * E] = (uint32_t)rd;
+        ea_posp[(int64_t)tstep * E] = ea_p0 + (uint32_t)rd;
         wrap = tstep + 1 < T_s ? 1 : 0;
         tstep += wrap;
       }
@@ -879,7 +896,7 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
     if constexpr (EA) {
       if (((has_q | new_order) ^ 1) & (r + 1 == R ? 1 : 0)) {
         ea_offp[(int64_t)(tstep + 1) * E] = n;
-        ea_posp[(int64_t)tstep * E] = (uint32_t)rd;
+        ea_posp[(int64_t)tstep * E] = ea_p0 + (uint32_t)rd;
         wrap = tstep + 1 < T_s ? 1 : 0;
         tstep += wrap;
       }
@@ -1733,7 +1750,7 @@ static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t 
   }
   const UFn fn = c.demand_uni ? (UFn)demand_unit_kernel<K, G, false, true, false>
                               : (t ? (UFn)demand_unit_kernel<K, G, true, false, false> : (UFn)demand_unit_kernel<K, G, false, false, false>);
-  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), lds, st, d, EaLaunch{0, 0, 0, 0});
+  hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), lds, st, d, EaLaunch{0, 0, 0, 0, 0, 0, 0});
 }
 
 template <int K>

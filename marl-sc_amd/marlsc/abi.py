@@ -121,6 +121,9 @@ def lib() -> C.CDLL:
                                         vp, vp, vp, C.c_int32, vp]
     L.msc_mlp2_relu_forward.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp,
                                         C.c_int32, vp]
+    L.msc_meanstd_scratch_doubles.argtypes = [C.c_int64, C.c_int32]
+    L.msc_meanstd_scratch_doubles.restype = C.c_int64
+    L.msc_meanstd_filter.argtypes = [vp, vp, C.c_int64, C.c_int32, vp, C.c_int32, vp, vp, C.c_double, C.c_double, vp]
     L.msc_seedseq_u32.argtypes = [P(C.c_uint32), C.c_int32]
     L.msc_seedseq_u32.restype = C.c_uint32
     L.msc_last_error.restype = C.c_char_p
@@ -140,5 +143,6 @@ def check(rc: int) -> None:
 EXPORTED_SYMBOLS = [
     "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_timing", "msc_env_read_timing", "msc_env_read_timing_ea", "msc_env_obs_flat",
     "msc_env_read_state", "msc_env_state_bytes", "msc_env_save_state", "msc_env_load_state", "msc_env_check",
-    "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_w3_layout", "msc_mlp3_relu_forward", "msc_mlp2_relu_forward", "msc_seedseq_u32", "msc_last_error", "msc_abi_version",
+    "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_w3_layout", "msc_mlp3_relu_forward", "msc_mlp2_relu_forward",
+    "msc_meanstd_scratch_doubles", "msc_meanstd_filter", "msc_seedseq_u32", "msc_last_error", "msc_abi_version",
 ]

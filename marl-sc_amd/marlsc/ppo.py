@@ -25,7 +25,10 @@ tests check the loss against a direct restatement and the training loop's invari
 * learning-rate schedules: [[timestep, lr], ...] piecewise linear in sampled env steps;
 * observation statistics for meanstd_custom / meanstd_grouped: src/utils/obs_stats.py:11-169,
   the random-policy episodes run on the GPU env (same seeds, same action stream, bit-exact obs),
-  the statistics on the host with numpy exactly as the reference computes them.
+  the statistics on the host with numpy exactly as the reference computes them;
+* obs_normalization "meanstd": RLlib's running MeanStdFilter connector (mappo.py:170-171) on the
+  device, synchronised after every rollout and applied with update=False in evaluation
+  (base.py:131-140; marlsc/obs_filter.py).
 
 Multi-GPU: each rank steps its own env shard (global env ids, marlsc/dist.py), the advantage
 statistics and the gradients (one flat f32 buffer per minibatch) are all-reduced -- RCCL over xGMI
@@ -111,9 +114,9 @@ class PPOConfig:
             raise ValueError("clip_param should typically be <= 1.0")
         if c.hysteretic_beta is not None and not (0.0 < c.hysteretic_beta <= 1.0):
             raise ValueError("hysteretic_beta must be in (0.0, 1.0]")
-        if c.obs_normalization == "meanstd":
-            raise ValueError("obs_normalization 'meanstd' (RLlib's running MeanStdFilter connector) is not in this "
-                             "build; use meanstd_custom / meanstd_grouped")
+        if c.obs_normalization not in ("off", "ratio", "meanstd", "meanstd_custom", "meanstd_grouped"):
+            raise ValueError(f"obs_normalization '{c.obs_normalization}' is not one of off / ratio / meanstd / "
+                             "meanstd_custom / meanstd_grouped")
         return c
 
     def rollout_config(self) -> RolloutConfig:
@@ -500,7 +503,8 @@ class PPOTrainer:
         # advantages standardised per module (RLlib's GAE connector): one group for the shared policy,
         # one per agent otherwise
         self.collector = RolloutCollector(self.env, self.module, self.T, seed=self.train_seed + 1000 + self.rank,
-                                          adv_groups=1 if cfg.parameter_sharing else W)
+                                          adv_groups=1 if cfg.parameter_sharing else W,
+                                          obs_filter="meanstd" if cfg.obs_normalization == "meanstd" else "off")
         self.env.reset()
         self.iteration = 0
         self.timesteps = 0
@@ -573,8 +577,11 @@ class PPOTrainer:
         env.set_episode_counters(np.arange(n, dtype=np.int32))
         obs = env.reset()
         full_fn = self._full_fn()
+        filt = self.collector.obs_filter  # "meanstd": the trained filter with update=False
         ret = torch.zeros(n, dtype=torch.float64, device=self.device)
         for _ in range(spec.episode_length):
+            if filt is not None:
+                obs = filt.normalize(obs)
             full = env.obs_flat(obs=obs) if full_fn is not None else None
             mean, _ = self.module.dist_inputs(obs, full)
             obs, rew, trunc, _ = env.step(mean.clamp(-1.0, 1.0).contiguous())
@@ -594,9 +601,11 @@ class PPOTrainer:
         p = Path(path)
         p.mkdir(parents=True, exist_ok=True)
         if self.rank == 0:
+            filt = self.collector.obs_filter
             torch.save({"module": self.module.state_dict(), "optimizer": self.learner.opt.state_dict(),
                         "kl_coeffs": list(self.learner.kl_coeffs), "iteration": self.iteration,
-                        "timesteps": self.timesteps}, p / "learner_state.pt")
+                        "timesteps": self.timesteps,
+                        "obs_filter": None if filt is None else filt.state_dict()}, p / "learner_state.pt")
             stats = self.env_meta.get("obs_stats")
             (p / "state.json").write_text(json.dumps({
                 "iteration": self.iteration, "timesteps": self.timesteps, "root_seed": self.root_seed,
@@ -608,7 +617,9 @@ class PPOTrainer:
                     "obs": self.env.obs.detach().cpu(), "t_sync": int(getattr(self.env, "_t_sync", -1)),
                     "rollout_gen": self.collector._gen.get_state(), "learner_gen": self.learner.gen.get_state(),
                     "ep_ret": self._ep_ret.detach().cpu(), "completed": list(self._completed),
-                    "n_episodes": self._n_episodes}, p / f"runtime_rank{self.rank}.pt")
+                    "n_episodes": self._n_episodes,
+                    "obs_filtered": [bool(ln.obs_filtered) for ln in self.collector._lanes]},
+                   p / f"runtime_rank{self.rank}.pt")
         return p
 
     def export_module_weights(self, path: Union[str, Path]) -> Path:
@@ -640,6 +651,10 @@ class PPOTrainer:
             self.learner.kl_coeffs = [float(st["kl_coeff"])] * len(self.module.policies)
         self.iteration = int(st["iteration"])
         self.timesteps = int(st["timesteps"])
+        if self.collector.obs_filter is not None:
+            if st.get("obs_filter") is None:
+                raise ValueError(f"{p}: obs_normalization 'meanstd' but the checkpoint holds no filter state")
+            self.collector.obs_filter.load_state_dict(st["obs_filter"])
         rt_path = p / f"runtime_rank{self.rank}.pt"
         if not runtime or not rt_path.exists():  # module-only checkpoint: weights restored, sampling restarts
             return
@@ -652,3 +667,5 @@ class PPOTrainer:
         self._ep_ret.copy_(rt["ep_ret"].to(self.device))
         self._completed = deque((float(x) for x in rt["completed"]), maxlen=self._completed.maxlen)
         self._n_episodes = int(rt["n_episodes"])
+        for ln, f in zip(self.collector._lanes, rt.get("obs_filtered", [])):
+            ln.obs_filtered = bool(f)

@@ -231,6 +231,7 @@ class _Lane:
     def __init__(self, env: VecInventoryEnv, e0: int, stream: Optional[torch.cuda.Stream], flat: Optional[torch.Tensor]):
         self.env, self.e0, self.e1, self.stream, self.flat = env, e0, e0 + env.n_envs, stream, flat
         self.noise: Optional[torch.Tensor] = None
+        self.obs_filtered = False  # the env's current observation already went through the obs filter
 
     def ctx(self):
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
@@ -247,7 +248,8 @@ class RolloutCollector:
     is the concatenation of the lanes; each env's trajectory is the same as with one handle (envs
     are independent and seeded by global id), the Gaussian noise differs (drawn per lane)."""
 
-    def __init__(self, env, module: ActorCritic, T: int, *, seed: int = 0, adv_groups: int = 1):
+    def __init__(self, env, module: ActorCritic, T: int, *, seed: int = 0, adv_groups: int = 1,
+                 obs_filter: str = "off"):
         envs = list(env) if isinstance(env, (list, tuple)) else [env]
         e0 = envs[0]
         for x in envs[1:]:
@@ -277,6 +279,14 @@ class RolloutCollector:
         self.stats = torch.zeros((self.adv_groups, 3), dtype=torch.float64, device=dev)
         self._need_flat = module.rc.actor_obs_type == "global"  # the critic splits its first layer
         self._gen = torch.Generator(device=dev).manual_seed(seed)
+        # obs_normalization "meanstd": RLlib's running filter, one per lane (env runner), synchronised
+        # after every collect (marlsc/obs_filter.py)
+        self.obs_filter = None
+        if obs_filter == "meanstd":
+            from .obs_filter import MeanStdObsFilter
+            self.obs_filter = MeanStdObsFilter(W * L, dev, n_lanes=len(envs))
+        elif obs_filter not in ("off", None):
+            raise ValueError(f"obs_filter must be 'off' or 'meanstd', not {obs_filter!r}")
         self._lanes, off = [], 0
         for x in envs:
             st = torch.cuda.Stream(device=dev) if len(envs) > 1 else None
@@ -304,6 +314,11 @@ class RolloutCollector:
         a = gaussian_sample(mean.contiguous(), log_std[0], m.rc.logstd_floor, eps, self.actions[t, sl], self.logp[t, sl])
         may_end = env.may_truncate()
         _, _, trunc, final_obs = env.step(a, obs_out=self._obs_all[t + 1, sl], rewards_out=self.rewards[t, sl])
+        li = self._lanes.index(ln) if self.obs_filter is not None else 0
+        if self.obs_filter is not None:  # the new observations first, then the truncated envs' final ones
+            self.obs_filter.apply(li, self._obs_all[t + 1, sl])
+            if may_end:
+                self.obs_filter.apply(li, final_obs, mask=trunc)
         self.truncated[t, sl] = trunc.unsqueeze(-1)
         # truncation bootstrap: V(final_obs) for the envs whose episode ended at this step
         # (skipped while the envs are known to be mid-episode in lockstep; next_values is zeroed
@@ -328,6 +343,9 @@ class RolloutCollector:
                 ln.stream.wait_stream(main)
             with ln.ctx():
                 self._obs_all[0, ln.e0:ln.e1].copy_(ln.env.obs)
+                if self.obs_filter is not None and not ln.obs_filtered:  # the reset observation
+                    self.obs_filter.apply(self._lanes.index(ln), self._obs_all[0, ln.e0:ln.e1])
+                ln.obs_filtered = True
         # lanes interleaved per step on the host; each lane's chain is ordered on its own stream
         for t in range(T):
             for ln in self._lanes:
@@ -340,6 +358,8 @@ class RolloutCollector:
                 ln.env.obs.copy_(last)  # the env's own buffer holds the current observation again
             if ln.stream is not None:
                 main.wait_stream(ln.stream)
+        if self.obs_filter is not None:
+            self.obs_filter.sync()
         N = self.N
         gae(self.rewards.view(T, N), self.values.view(T + 1, N), self.next_values.view(T, N),
             self.terminated.view(T, N), self.truncated.view(T, N), m.rc.gamma, m.rc.lam,

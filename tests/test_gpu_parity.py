@@ -467,13 +467,17 @@ def test_empirical_trace_demand_vs_oracle(W, R, lost):
     _lockstep(spec, 96, 14, seed=4, check_every=3)
 
 
-def test_episode_ahead_equals_sequential(monkeypatch):
+@pytest.mark.parametrize("slots,batch,chunk", [(4, 1, 10), (4, 2, 2), (6, 2, 4)])
+def test_episode_ahead_equals_sequential(monkeypatch, slots, batch, chunk):
     # episode-ahead demand (whole future episodes drawn on a side stream)
     # against per-step sequential demand: identical observations, rewards and reported state
     # (PCG64 demand stream included) across episode boundaries, save/load in the middle of a
-    # generated episode, a full reset mid-episode, a masked reset and episode-counter rewrites
+    # generated episode, a full reset mid-episode, a masked reset and episode-counter rewrites;
+    # refills of `batch` slots per generation, generated in chunks of `chunk` steps (6-step episodes)
     monkeypatch.setenv("MSC_EA", "1")
-    monkeypatch.setenv("MSC_EA_SLOTS", "4")
+    monkeypatch.setenv("MSC_EA_SLOTS", str(slots))
+    monkeypatch.setenv("MSC_EA_BATCH", str(batch))
+    monkeypatch.setenv("MSC_EA_CHUNK", str(chunk))
     monkeypatch.setenv("MSC_ALLOC_IMPL", "scan")
     cfg = make_synthetic_env_config(8, 64, 5, episode_length=6)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
@@ -515,7 +519,7 @@ def test_episode_ahead_equals_sequential(monkeypatch):
                 assert np.array_equal(sa[k], sb[k]), f"{k} at step {t}"
     assert seen_active
     tm = a.read_timing_ea()
-    assert tm["slots"] == 4 and tm["n_ea"] > 0 and tm["ea_ms"] > 0
+    assert tm["slots"] == slots and tm["n_ea"] > 0 and tm["ea_ms"] > 0
     a.check()
     b.check()
 

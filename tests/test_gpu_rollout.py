@@ -274,3 +274,43 @@ def test_multi_lane_rollout_after_weight_update_uses_fresh_packs():
             for t in (0, 3, 5):
                 ref = m.critic(col.obs[t]).squeeze(-1).detach()
                 torch.testing.assert_close(col.values[t], ref, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("E", [1, 37, 300, 5000])
+def test_meanstd_filter_kernel_matches_the_oracle(E):
+    # obs_normalization "meanstd" (RLlib's MeanStdFilter connector, mappo.py:170-171): the device
+    # filter (segments of sequential pushes joined by Chan merges) against the numpy restatement's
+    # strictly sequential pushes over several steps, a masked push (final observations) and an
+    # update=False pass; f32 outputs to rounding, f64 statistics to 1e-10
+    from meanstd_ref import MeanStdFilter, filter_rows
+    from marlsc.obs_filter import MeanStdObsFilter
+    W, L = 3, 7
+    C = W * L
+    rng = np.random.default_rng(E)
+    dev = MeanStdObsFilter(C, "cuda", n_lanes=1)
+    ref = MeanStdFilter((C,))
+    scale = rng.uniform(0.1, 50.0, C)
+    for step in range(4):
+        x = (rng.normal(2.0, 1.0, (E, W, L)) * scale.reshape(W, L)).astype(np.float32)
+        xt = torch.from_numpy(x).cuda()
+        mask = None
+        if step == 2:
+            mask = (rng.uniform(size=E) < 0.5).astype(np.uint8)
+            mask[0] = 1
+        got = dev.apply(0, xt, mask=None if mask is None else torch.from_numpy(mask).cuda())
+        want = filter_rows(ref, x.reshape(E, C), mask=mask)
+        np.testing.assert_allclose(got.reshape(E, C).cpu().numpy(), want, rtol=1e-5, atol=1e-5)
+    st = dev.lanes[0].cpu().numpy()
+    assert st[0] == ref.rs.n and st[1] == ref.buffer.n
+    np.testing.assert_allclose(st[4:4 + C], ref.rs.M, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(st[4 + C:4 + 2 * C], ref.rs.S, rtol=1e-10)
+    np.testing.assert_allclose(st[4 + 2 * C:4 + 3 * C], ref.buffer.M, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(st[4 + 3 * C:], ref.buffer.S, rtol=1e-10)
+    # synchronisation: the driver takes the buffer; evaluation normalises without pushing
+    dev.sync()
+    assert dev.count == ref.rs.n and float(dev.lanes[0][1]) == 0.0
+    x = rng.normal(0, 3.0, (E, W, L)).astype(np.float32)
+    got = dev.normalize(torch.from_numpy(x).cuda())
+    want = filter_rows(ref, x.reshape(E, C), update=False)
+    np.testing.assert_allclose(got.reshape(E, C).cpu().numpy(), want, rtol=1e-5, atol=1e-5)
+    assert dev.count == ref.rs.n

@@ -214,3 +214,32 @@ def test_per_agent_policies_standardise_advantages_per_agent():
     torch.testing.assert_close(adv.mean(0), torch.zeros(W, dtype=torch.float64, device=adv.device), atol=1e-4, rtol=0)
     torch.testing.assert_close(adv.std(0, unbiased=False), torch.ones(W, dtype=torch.float64, device=adv.device),
                                atol=1e-3, rtol=0)
+
+
+def test_meanstd_running_filter_training_evaluation_and_checkpoint(tmp_path):
+    # obs_normalization "meanstd": RLlib's running filter on the device -- every observation the
+    # policy sees is pushed once (reset observation, each step's, the final observation of every
+    # truncated episode), the lanes synchronise after each rollout, evaluation applies it without
+    # updating, and checkpoints carry it
+    from marlsc.ppo import PPOTrainer
+    E, T = 64, 8
+    tr, env_cfg, cfg = _trainer("mappo", True, E=E, T=T, obs_normalization="meanstd")
+    for _ in range(2):
+        res = tr.train_iteration()
+        assert np.isfinite(res["learner/total_loss"])
+    f = tr.collector.obs_filter
+    # 16 steps of 10-step episodes: E reset obs + 16 E step obs + E final obs (the truncation at step 10)
+    assert f.count == E + 2 * T * E + E
+    assert float(tr.collector.obs.abs().max()) <= 10.0
+    assert float(f.std.min()) >= 0.0 and torch.isfinite(f.mean).all()
+    ev = tr.evaluate()
+    assert np.isfinite(ev["eval/episode_return_mean"]) and f.count == E + 2 * T * E + E
+    assert tr.evaluate() == ev
+    ck = tr.save_checkpoint(tmp_path / "ck")
+    tr2 = PPOTrainer(env_cfg, cfg, root_seed=7, n_envs=E, rollout_len=T, device=0)
+    tr2.load_checkpoint(ck)
+    assert torch.equal(tr2.collector.obs_filter.driver, f.driver)
+    assert tr2.evaluate() == ev
+    tr.train_iteration()
+    tr2.train_iteration()
+    assert tr2.collector.obs_filter.count == tr.collector.obs_filter.count

@@ -43,8 +43,9 @@ def test_algorithm_configs_parse_like_the_reference_schema():
         PPOConfig.from_algorithm_config({"algorithm": {"name": "cppo", "shared": {}, "algorithm_specific": {}}})
     with pytest.raises(ValueError):
         _cfg("mappo", hysteretic_beta=1.5)
+    assert _cfg("mappo", obs_normalization="meanstd").obs_normalization == "meanstd"  # RLlib's running filter
     with pytest.raises(ValueError):
-        _cfg("mappo", obs_normalization="meanstd")
+        _cfg("mappo", obs_normalization="zscore")
 
 
 def test_learning_rate_schedule_is_piecewise_linear():
