@@ -170,10 +170,10 @@ def c2_line(args, rank: int):
                        f"(BASELINE configs[1])",
            "value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "ms_per_step": round(dt / steps * 1e3, 4),
            "steps": steps, "warmup": warm, "obs_normalization": norm,
-           "demand": (f"episode-ahead: whole episodes drawn on a side stream, {tm['slots']} slots per env"
-                      if tm["slots"] else "per step (pipelined)"),
+           "demand": (f"episode-ahead: future episodes drawn on a side stream ({tm['slots']} slots per env, "
+                      f"generated in 10-step chunks, several slots per launch)" if tm["slots"] else "per step (pipelined)"),
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
-                          "demand_ea_kernel_per_episode": round(tm["ea_ms"], 4) if tm["n_ea"] else None,
+                          "demand_ea_chunk": round(tm["ea_ms"], 4) if tm["n_ea"] else None,
                           "demand_per_step": round(tm["demand_ms"], 4) if tm["n_demand"] else None}}
     if args.rollout_T > 0:
         out["rollout"] = {"value": round(E * spec.W * T / t_roll, 1), "unit": "agent-steps/s",

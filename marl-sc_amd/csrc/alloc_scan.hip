@@ -314,6 +314,9 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   SPROF(n_epi);
   SPROF(n_bat);
   SPROF_T(t_begin);
+#ifdef MSC_PROF
+  const unsigned long long rt_begin = (unsigned long long)wall_clock64();  // constant-rate (100 MHz) clock
+#endif
   uint4 nxt = lane < n ? gload4(src, o.base + (int64_t)lane * o.nstep) : make_uint4(0u, 0u, 0u, 0u);
   for (int o0 = 0; o0 < n; o0 += SC_WIN) {
     const int nw = n - o0 < SC_WIN ? n - o0 : SC_WIN;
@@ -441,6 +444,9 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   SPROF_FLUSH(4, (unsigned long long)n);
   SPROF_FLUSH(5, 1ull);
   SPROF_FLUSH(6, n_bat);
+#ifdef MSC_PROF
+  SPROF_FLUSH(7, (unsigned long long)wall_clock64() - rt_begin);
+#endif
 
   // penalty (reward_calculator.py:134-137): (lost_sales * per-SKU cost, or * sku_weights * cost)
   // summed over SKUs in order; outbound variable cost: sum over SKUs of sku_weight * ovacc

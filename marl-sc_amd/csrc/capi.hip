@@ -397,7 +397,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     const char* prot = getenv("MSC_PARSER_ROT");
     c.parser_rot = prot ? atoi(prot) : 0;
     // step_c observation staging when the block's stage fits (C3: 8 x 64 x 35 floats = 70 KiB)
-    c.obs_stage = (size_t)c.W * BS * (c.L + 1) * sizeof(float) <= 80 * 1024 ? 1 : 0;
+    c.obs_stage = (size_t)BS * ((c.W * c.L) | 1) * sizeof(float) <= 80 * 1024 ? 1 : 0;
     if (const char* os = getenv("MSC_OBS_STAGE")) c.obs_stage = c.obs_stage && atoi(os) != 0;
     // phase B: one env per lane (alloc_lane_kernel) when there are enough env chains to fill the
     // chip and the Poisson demand kernel of the next step runs beside it (it then needs the issue

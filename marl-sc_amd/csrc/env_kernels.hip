@@ -163,7 +163,7 @@ __device__ __noinline__ void reset_env(const EnvConst& c, const EnvState& s, int
 //   shh/sht are indexed [(w * K + sku) * BS] from a pointer already offset to the env's column.
 // One agent (warehouse w) per call: the step kernel builds the W agents of an env in parallel.
 template <int K>
-__device__ __noinline__ void build_obs_agent(const EnvConst& c, const EnvState& s, int64_t e, int w, int t_now,
+__device__ __forceinline__ void build_obs_agent(const EnvConst& c, const EnvState& s, int64_t e, int w, int t_now,
                                              int n_hist, const int32_t* shh, const int32_t* sht, int64_t sstride,
                                              float* out) {
   const int64_t E = c.E;
@@ -1625,12 +1625,13 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __
   __syncthreads();
   bool trunc = false;
   const int64_t obs_off = e * W * c.L;
-  // observation staging: this wave's 64 agents' vectors [lane][L + 1] (odd stride), written to
-  // HBM afterwards as runs of consecutive floats (a lane's own vector is L floats at a stride of
-  // W*L floats from the next env's: storing it directly leaves 64 partially written lines per
-  // store instruction, ~5x the algorithmic write bytes in the PMC counters)
-  const int L = c.L;
-  float* stg = reinterpret_cast<float*>(Lrw + W * BS) + (int64_t)wave * BS * (L + 1);
+  // observation staging: the block's 64 envs x W agents' vectors [env][W*L] (row stride W*L | 1,
+  // odd: a wave's 64 lanes write 64 different banks), then written to HBM as the block's one
+  // contiguous [64][W][L] range, every cache line whole (per-agent vectors of L floats at a
+  // stride of W*L floats leave partly written lines per store)
+  const int L = c.L, WL = W * L, RS = WL | 1;
+  float* stg = reinterpret_cast<float*>(Lrw + W * BS);
+  int32_t* Lskip = reinterpret_cast<int32_t*>(stg + BS * RS);  // [BS]: env's vector not staged
   // shipped home / total of this step, [(w*K+s) * E] from the env's column
   const int32_t* shh = s.sc_shh + e;
   const int32_t* sht = s.sc_sht + e;
@@ -1645,26 +1646,26 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __
     const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
     trunc = t + 1 >= c.T;
     if (!trunc) {
-      build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E,
-                         c.obs_stage ? stg + lane * (L + 1) - (int64_t)w * L : io.obs + obs_off);
+      build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, c.obs_stage ? stg + lane * RS : io.obs + obs_off);
     } else if (io.final_obs) {
       build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
     }
   }
-  if (c.obs_stage && wave < W) {
-    // copy-out: flat index i = env * L + j over the wave's 64 vectors, 64 consecutive i per store
-    const uint64_t skip = __ballot(!act || trunc);  // envs whose vector is not in the stage
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int q = BS / L, rr = BS % L;
-    int ev = lane / L, j = lane % L;
+  if (c.obs_stage) {
+    if (wave == 0) Lskip[lane] = (e >= E || trunc) ? 1 : 0;
+    __syncthreads();
     const int64_t e0 = (int64_t)blockIdx.x * BS;
-    for (int it = 0; it < L; it++) {
-      if (!((skip >> ev) & 1ull)) io.obs[((e0 + ev) * W + w) * L + j] = stg[ev * (L + 1) + j];
-      j += rr;
-      ev += q;
-      if (j >= L) {
-        j -= L;
+    const int nenv = E - e0 < BS ? (int)(E - e0) : BS;
+    const int n = nenv * WL, nt = (int)blockDim.x;
+    const int dq = nt / WL, dr = nt % WL;  // (env, column) step of the flat index per iteration
+    int ev = (int)threadIdx.x / WL, j = (int)threadIdx.x % WL;
+    float* dst = io.obs + e0 * WL;
+    for (int i = (int)threadIdx.x; i < n; i += nt) {
+      if (!Lskip[ev]) dst[i] = stg[ev * RS + j];
+      j += dr;
+      ev += dq;
+      if (j >= WL) {
+        j -= WL;
         ev += 1;
       }
     }
@@ -1807,7 +1808,8 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     if (c.alloc_sort) hipLaunchKernelGGL(alloc_sort_kernel, dim3(1), dim3(1024), 0, st, d, io);
     hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
   }
-  const size_t lds_c = (size_t)c.W * BS * sizeof(double) + (c.obs_stage ? (size_t)c.W * BS * (c.L + 1) * sizeof(float) : 0);
+  const size_t lds_c = (size_t)c.W * BS * sizeof(double) +
+                       (c.obs_stage ? (size_t)BS * ((c.W * c.L) | 1) * sizeof(float) + BS * sizeof(int32_t) : 0);
   hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), lds_c, st, d, io);
   return hipGetLastError();
 }

@@ -14,13 +14,22 @@ import sys
 tag = sys.argv[1]
 workload = sys.argv[2] if len(sys.argv) > 2 else "8x64x5x32768"
 out = collections.defaultdict(dict)
+# dispatches are grouped by kernel and grid size; per kernel only the largest grid (the workload's
+# launches, not those of the small helper envs bench.py builds, e.g. for observation statistics)
+grids = collections.defaultdict(set)
 for path in glob.glob(f"gpurun_out/pmc_*_{tag}/**/*counter_collection.csv", recursive=True):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for row in csv.DictReader(open(path)):
-        acc[row["Kernel_Name"].split("(")[0]][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    for k, v in acc.items():
+        name = row["Kernel_Name"].split("(")[0]
+        grid = int(float(row.get("Grid_Size", 0) or 0))
+        grids[name].add(grid)
+        acc[(name, grid)][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    for (name, grid), v in acc.items():
+        if grid != max(grids[name]):
+            continue
         for c, x in v.items():
-            out[k][c] = sum(x) / len(x)
+            out[name][c] = sum(x) / len(x)
+        out[name]["grid_size"] = grid
 traffic = {}
 counters = {}
 for k, v in sorted(out.items()):

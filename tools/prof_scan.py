@@ -43,3 +43,6 @@ print(f"per wave: cycles {v[0] / w:.0f}, ranking {v[1] / w:.0f}, epilogues {v[2]
       f"orders {v[4] / w:.1f}; chain cycles per order (excl. ranking, epilogues) "
       f"{(v[0] - v[1] - v[2]) / max(v[4], 1):.0f}; cycles per epilogue {v[2] / max(v[3], 1):.0f}; "
       f"batches {v[6] / w:.1f} ({v[4] / max(v[6], 1):.2f} orders each)")
+if v[7]:
+    print(f"shader clock while the loop ran: {v[0] / v[7] * 100:.0f} MHz (clock64 cycles / 100 MHz wall-clock ticks), "
+          f"loop wall {v[7] / w / 100:.1f} us per wave")
