@@ -175,6 +175,24 @@ def c2_line(args, rank: int):
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
                           "demand_ea_chunk": round(tm["ea_ms"], 4) if tm["n_ea"] else None,
                           "demand_per_step": round(tm["demand_ms"], 4) if tm["n_demand"] else None}}
+    # the step kernels against the VALU issue peak: PMC instruction counts of the same workload
+    # (scripts/gpu_profile.sh -> profiles/traffic.json) over the live step-kernel time
+    tj = Path(args.traffic_json)
+    if tj.exists():
+        tr = json.loads(tj.read_text())
+        key = f"{spec.W}x{spec.R}x{spec.K}x{E}"
+        names = ("step_a_kernel", "alloc_scan_kernel", "step_c_kernel")
+        cn = [tr.get("counters", {}).get(key, {}).get(n, {}).get("SQ_INSTS_VALU") for n in names]
+        tb = [tr.get(key, {}).get(n) for n in names]
+        if all(x is not None for x in cn) and tm["step_ms"] > 0:
+            ach = sum(cn) / (tm["step_ms"] * 1e-3)
+            out["roofline"] = {"kernel": "step_kernels (step_a + alloc_scan + step_c)", "bound": "valu issue",
+                               "insts_per_step": int(sum(cn)), "achieved": round(ach / 1e9, 2),
+                               "peak": round(VALU_PEAK_WINST / 1e9, 1), "unit": "G wave-instructions/s",
+                               "frac": round(ach / VALU_PEAK_WINST, 4),
+                               "traffic": sum(tb) if all(x is not None for x in tb) else None,
+                               "note": "one env per wave in the allocation (4 waves per SIMD at 4,096 envs): "
+                                       "issue-bound per SIMD, DESIGN.md section 3"}
     if args.rollout_T > 0:
         out["rollout"] = {"value": round(E * spec.W * T / t_roll, 1), "unit": "agent-steps/s",
                           "ms_per_step": round(t_roll / T * 1e3, 4), "T": T,
@@ -413,6 +431,14 @@ def main():
                 valu = {"insts_per_launch": int(sum(cn)), "achieved": round(ach / 1e9, 2),
                         "peak": round(VALU_PEAK_WINST / 1e9, 1), "unit": "G wave-instructions/s",
                         "frac": round(ach / VALU_PEAK_WINST, 4)}
+                # the kernel's effective clock under load (GRBM_GUI_ACTIVE / 8 / wall, PMC pass): a
+                # wave64 VALU instruction takes 4 cycles of a SIMD, so the issue peak at that clock is
+                # 1024 SIMDs x clock / 4
+                clk = [tr.get("clock_mhz", {}).get(key, {}).get(n) for n in names]
+                if len(names) == 1 and clk[0]:
+                    pk = 1024 * clk[0] * 1e6 / 4
+                    valu.update({"clock_mhz": clk[0], "peak_at_clock": round(pk / 1e9, 1),
+                                 "frac_at_clock": round(ach / pk, 4)})
         # the whole pipelined step against the same issue peak: every kernel of a step (demand of
         # t + 1 and the step kernels of t run concurrently) over the measured time per step
         step_valu = None

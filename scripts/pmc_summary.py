@@ -44,4 +44,22 @@ for k, v in sorted(out.items()):
         print(f"   => HBM traffic per launch {traffic[m.group(1)] / 1e6:.2f} MB (2 x FETCH + WRITE)")
     if m:
         counters[m.group(1)] = {c: v[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES") if c in v}
-json.dump({workload: traffic, "counters": {workload: counters}}, open(f"gpurun_out/traffic_{tag}.json", "w"), indent=1)
+# effective shader clock per kernel: GRBM_GUI_ACTIVE counts busy cycles summed over the 8 XCDs
+# (MI355X_MICROARCH.md), divided by the kernel's mean duration at the same grid (kernel trace)
+clocks = {}
+dur = {}
+try:
+    for row in csv.DictReader(open(f"gpurun_out/kernel_stats_by_grid_{tag}.csv")):
+        name = row["Name"].split("(")[0]
+        g = int(row["Grid_Size"])
+        if name not in dur or g > dur[name][0]:
+            dur[name] = (g, float(row["AverageNs"]))
+except FileNotFoundError:
+    pass
+for k, v in out.items():
+    m = re.search(r"msc::(\w+)", k)
+    if m and "GRBM_GUI_ACTIVE" in v and k in dur and dur[k][1] > 0:
+        clocks[m.group(1)] = round(v["GRBM_GUI_ACTIVE"] / 8 / dur[k][1] * 1e3, 1)  # MHz
+        print(f"{k}: effective clock {clocks[m.group(1)]} MHz (GRBM_GUI_ACTIVE / 8 / {dur[k][1] / 1e3:.1f} us)")
+json.dump({workload: traffic, "counters": {workload: counters}, "clock_mhz": {workload: clocks}},
+          open(f"gpurun_out/traffic_{tag}.json", "w"), indent=1)
