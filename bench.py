@@ -422,7 +422,9 @@ def main():
         key = f"{spec.W}x{spec.R}x{spec.K}x{E}"
         if tj.exists():
             tr = json.loads(tj.read_text())
-            names = STEP_KERNELS if dom == "step_kernels" else (dom,)
+            # the phase kernels this workload ran (allocation: lane / group (+ order sort) / scan)
+            step_names = tuple(n for n in tr.get(key, {}) if n not in (DEMAND_KERNEL, DEMAND_KERNEL + "_ea", "reset_kernel"))
+            names = (step_names or STEP_KERNELS) if dom == "step_kernels" else (dom,)
             tb = [tr.get(key, {}).get(n) for n in names]
             traffic = sum(tb) if all(x is not None for x in tb) else None
             cn = [tr.get("counters", {}).get(key, {}).get(n, {}).get("SQ_INSTS_VALU") for n in names]
@@ -444,7 +446,7 @@ def main():
         step_valu = None
         if tj.exists():
             cs = tr.get("counters", {}).get(key, {})
-            names_all = (DEMAND_KERNEL,) + STEP_KERNELS
+            names_all = ((DEMAND_KERNEL,) if DEMAND_KERNEL in cs else ()) + (step_names or STEP_KERNELS)
             vals = [cs.get(n, {}).get("SQ_INSTS_VALU") for n in names_all]
             if all(x is not None for x in vals):
                 ach_s = sum(vals) / (dt / K)

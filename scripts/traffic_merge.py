@@ -13,18 +13,18 @@ src, key, note = sys.argv[1], sys.argv[2], sys.argv[3]
 out_path = Path(sys.argv[4] if len(sys.argv) > 4 else Path(__file__).resolve().parents[1] / "profiles" / "traffic.json")
 kern, vals, clocks = None, {}, {}
 for line in open(src):
-    m = re.match(r"^void msc::(\w+)<(.*)>\s*$", line.rstrip())
+    m = re.match(r"^(?:void )?msc::(\w+)(?:<(.*)>)?\s*$", line.rstrip())
     if m:
         name = m.group(1)
-        if name == "demand_unit_kernel" and m.group(2).replace(" ", "").endswith(",true"):
+        if name == "demand_unit_kernel" and (m.group(2) or "").replace(" ", "").endswith(",true"):
             name += "_ea"
         kern = name
         vals[kern] = {}
         continue
-    m = re.match(r"^void msc::(\w+)<(.*)>: effective clock ([\d.]+) MHz", line)
+    m = re.match(r"^(?:void )?msc::(\w+)(?:<(.*)>)?: effective clock ([\d.]+) MHz", line)
     if m:
         name = m.group(1)
-        if name == "demand_unit_kernel" and m.group(2).replace(" ", "").endswith(",true"):
+        if name == "demand_unit_kernel" and (m.group(2) or "").replace(" ", "").endswith(",true"):
             name += "_ea"
         clocks[name] = float(m.group(3))
         continue
