@@ -171,7 +171,7 @@ def c2_line(args, rank: int):
            "value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "ms_per_step": round(dt / steps * 1e3, 4),
            "steps": steps, "warmup": warm, "obs_normalization": norm,
            "demand": (f"episode-ahead: future episodes drawn on a side stream ({tm['slots']} slots per env, "
-                      f"generated in 10-step chunks, several slots per launch)" if tm["slots"] else "per step (pipelined)"),
+                      f"generated in 50-step chunks, several slots per launch)" if tm["slots"] else "per step (pipelined)"),
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
                           "demand_ea_chunk": round(tm["ea_ms"], 4) if tm["n_ea"] else None,
                           "demand_per_step": round(tm["demand_ms"], 4) if tm["n_demand"] else None}}

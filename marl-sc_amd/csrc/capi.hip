@@ -81,7 +81,7 @@ struct msc_env {
   // A generation runs as chunks of ea_chunk steps, each launched once the previous one has finished
   // (polled at every step call; flushed when a step needs the slot), so that the EA work queued on
   // the device at any time -- what a device-wide synchronize waits for -- is one short chunk.
-  int ea_chunk = 10;
+  int ea_chunk = 50;
   struct EaItem { EaLaunch l; int wait_cons; };  // wait_cons: slot whose ev_cons precedes chunk 0 (-1: none)
   std::vector<EaItem> ea_q;  // generations not yet fully launched (head: the one in progress)
   bool ea_chunk_out = false; // a chunk of the head item is in flight (ev_chunk)
@@ -612,7 +612,10 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       // after a chunk starts, none without staging): off with EA unless MSC_OBS_STAGE=1
       const char* os = getenv("MSC_OBS_STAGE");
       if (!(os && atoi(os) != 0)) c.obs_stage = 0;
-      int ch = 10;
+      // chunk A/B at C2 (scripts/gpu_ab_eachunk.sh, steps per launch -> M agent-steps/s): 5 -> 149.6,
+      // 10 -> 152.9, 20 -> 157.8, 34 -> 165.3, 50 -> 170.1, 100 -> 171.4 (fewer launch ramps and
+      // tails beside the step kernels); 50 keeps the work a synchronize may wait for at half an episode
+      int ch = 50;
       if (const char* ec = getenv("MSC_EA_CHUNK")) ch = atoi(ec);
       env->ea_chunk = ch < 1 ? 1 : ch;
     } else {
