@@ -93,9 +93,14 @@ def time_env(env, pool, steps: int, warmup: int, world: int):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if os.environ.get("BENCH_GC_FREEZE"):  # A/B: no Python GC pass over earlier objects in the loop
+        import gc
+        gc.collect()
+        gc.freeze()
     t0 = time.perf_counter()
     for i in range(steps):
         env.step(pool[i % len(pool)])
+    t_host = time.perf_counter() - t0  # the host's enqueue time (the device may still be busy)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -107,6 +112,7 @@ def time_env(env, pool, steps: int, warmup: int, world: int):
         env.step(pool[i % len(pool)])
     tm = env.read_timing()
     tm.update(env.read_timing_ea())
+    tm["host_ms_per_step"] = t_host / steps * 1e3
     env.set_timing(0)
     env.check()
     return dt, tm
@@ -156,10 +162,14 @@ def c2_line(args, rank: int):
     pool = [torch.rand((E, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
     env.reset()
     T = spec.episode_length
-    steps = max(args.steps, 10 * T)
-    # episode 0 of the episode-ahead snapshot draws its demand per step while the first S - 1
-    # episodes are generated; the slots refill in steady state after a few episodes
-    warm = 10 * T
+    # Episode-ahead demand refills 4 slots per launch, i.e. one generation launch per 4 episodes:
+    # a timed window of 1,000 steps held 2 or 3 of them depending on its phase (0.214 / 0.246 ms per
+    # step in consecutive windows, tools/ab_state.py), so the window is a whole number of refill
+    # periods (12 episodes = 3 periods), after a warm-up of the same length (episode 0 of the
+    # snapshot draws its demand per step while the first 11 episodes are generated)
+    period = 4 * T
+    steps = max(3 * period, -(-args.steps // period) * period)
+    warm = 3 * period
     dt, tm = time_env(env, pool, steps, warm, 1)
     rc = RolloutConfig.from_algorithm_config(algo)
     torch.manual_seed(0)
@@ -170,6 +180,7 @@ def c2_line(args, rank: int):
                        f"(BASELINE configs[1])",
            "value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "ms_per_step": round(dt / steps * 1e3, 4),
            "steps": steps, "warmup": warm, "obs_normalization": norm,
+           "host_ms_per_step": round(tm["host_ms_per_step"], 4),
            "demand": (f"episode-ahead: future episodes drawn on a side stream ({tm['slots']} slots per env, "
                       f"generated in 50-step chunks, several slots per launch)" if tm["slots"] else "per step (pipelined)"),
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
@@ -340,7 +351,8 @@ def main():
     # (4) the HBM-bound kernel of the rollout: msc_gae (GAE reverse scan + advantage statistics) over
     #     one MAPPO rollout's [T, E * W] sequences, timed alone with events on its stream
     gae_line = None
-    if rank == 0 and args.rollout_T > 0:
+    skip_micro = bool(os.environ.get("BENCH_SKIP_MICRO"))  # A/B knob
+    if rank == 0 and args.rollout_T > 0 and not skip_micro and not os.environ.get("BENCH_SKIP_GAE"):
         from marlsc.rollout import gae
         T, N = args.rollout_T, E * spec.W
         gg = torch.Generator(device="cuda").manual_seed(7)
@@ -371,7 +383,7 @@ def main():
     # (5) the MFMA-bound kernel of the rollout: the fused actor MLP (msc_mlp3_relu_forward) over one
     #     step's E * W rows, timed alone with events on its stream
     mlp_line = None
-    if rank == 0 and args.rollout_T > 0:
+    if rank == 0 and args.rollout_T > 0 and not skip_micro and not os.environ.get("BENCH_SKIP_MLP"):
         from marlsc.mlp import fusable, mlp3_forward
         mods = list(module.actor)
         if fusable(mods):
@@ -401,6 +413,17 @@ def main():
     c2 = None
     if world == 1 and args.c2_envs > 0 and args.config == "c3":
         env.close()
+        if os.environ.get("BENCH_C2_PAUSE"):  # A/B: idle seconds before the c2 line
+            time.sleep(float(os.environ["BENCH_C2_PAUSE"]))
+        if os.environ.get("BENCH_C2_FRAG"):  # A/B: fragment device memory (GB) before the c2 line
+            frag = [torch.empty(16 << 20, dtype=torch.uint8, device="cuda") for _ in range(int(float(os.environ["BENCH_C2_FRAG"]) * 64))]
+            del frag[::2]
+        if os.environ.get("BENCH_C2_EMPTY"):  # A/B: return torch's cached blocks first
+            import gc
+            if args.rollout_T > 0:
+                del module
+            gc.collect()
+            torch.cuda.empty_cache()
         c2 = c2_line(args, rank)
     tt = torch.tensor([dt, t_roll], dtype=torch.float64, device="cuda")
     if world > 1:

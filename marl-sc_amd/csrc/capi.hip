@@ -612,6 +612,11 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       // after a chunk starts, none without staging): off with EA unless MSC_OBS_STAGE=1
       const char* os = getenv("MSC_OBS_STAGE");
       if (!(os && atoi(os) != 0)) c.obs_stage = 0;
+      // the generation waves (parser 2, generators 1) are background work: the whole step chain
+      // runs above them (the allocation kernels are at 3 already; MSC_CHAIN_PRIO=0 leaves step_a /
+      // step_c at 0)
+      const char* cp = getenv("MSC_CHAIN_PRIO");
+      c.chain_prio = (cp && atoi(cp) == 0) ? 0 : 1;
       // chunk A/B at C2 (scripts/gpu_ab_eachunk.sh, steps per launch -> M agent-steps/s): 5 -> 149.6,
       // 10 -> 152.9, 20 -> 157.8, 34 -> 165.3, 50 -> 170.1, 100 -> 171.4 (fewer launch ramps and
       // tails beside the step kernels); 50 keeps the work a synchronize may wait for at half an episode
@@ -669,7 +674,11 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   }
   (void)hipEventRecord(env->ev_reset, env->side);
   if (env->ea_enabled) {
-    if (hipStreamCreateWithFlags(&env->ea_stream, hipStreamNonBlocking) != hipSuccess)
+    // MSC_EA_PRIO=low|high: queue priority of the generation stream (A/B; default: normal)
+    int ea_prio = 0, lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (const char* ep = getenv("MSC_EA_PRIO")) ea_prio = strcmp(ep, "low") == 0 ? lo : strcmp(ep, "high") == 0 ? hi : 0;
+    if (hipStreamCreateWithPriority(&env->ea_stream, hipStreamNonBlocking, ea_prio) != hipSuccess)
       return fail(set_err(-2, "EA stream creation failed"));
     for (int j = 0; j < MSC_EA_MAX_S; j++)
       if (hipEventCreateWithFlags(&env->ev_gen[j], hipEventDisableTiming) != hipSuccess ||
