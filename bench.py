@@ -93,10 +93,6 @@ def time_env(env, pool, steps: int, warmup: int, world: int):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if os.environ.get("BENCH_GC_FREEZE"):  # A/B: no Python GC pass over earlier objects in the loop
-        import gc
-        gc.collect()
-        gc.freeze()
     t0 = time.perf_counter()
     for i in range(steps):
         env.step(pool[i % len(pool)])
@@ -351,8 +347,7 @@ def main():
     # (4) the HBM-bound kernel of the rollout: msc_gae (GAE reverse scan + advantage statistics) over
     #     one MAPPO rollout's [T, E * W] sequences, timed alone with events on its stream
     gae_line = None
-    skip_micro = bool(os.environ.get("BENCH_SKIP_MICRO"))  # A/B knob
-    if rank == 0 and args.rollout_T > 0 and not skip_micro and not os.environ.get("BENCH_SKIP_GAE"):
+    if rank == 0 and args.rollout_T > 0:
         from marlsc.rollout import gae
         T, N = args.rollout_T, E * spec.W
         gg = torch.Generator(device="cuda").manual_seed(7)
@@ -383,7 +378,7 @@ def main():
     # (5) the MFMA-bound kernel of the rollout: the fused actor MLP (msc_mlp3_relu_forward) over one
     #     step's E * W rows, timed alone with events on its stream
     mlp_line = None
-    if rank == 0 and args.rollout_T > 0 and not skip_micro and not os.environ.get("BENCH_SKIP_MLP"):
+    if rank == 0 and args.rollout_T > 0:
         from marlsc.mlp import fusable, mlp3_forward
         mods = list(module.actor)
         if fusable(mods):
@@ -413,17 +408,6 @@ def main():
     c2 = None
     if world == 1 and args.c2_envs > 0 and args.config == "c3":
         env.close()
-        if os.environ.get("BENCH_C2_PAUSE"):  # A/B: idle seconds before the c2 line
-            time.sleep(float(os.environ["BENCH_C2_PAUSE"]))
-        if os.environ.get("BENCH_C2_FRAG"):  # A/B: fragment device memory (GB) before the c2 line
-            frag = [torch.empty(16 << 20, dtype=torch.uint8, device="cuda") for _ in range(int(float(os.environ["BENCH_C2_FRAG"]) * 64))]
-            del frag[::2]
-        if os.environ.get("BENCH_C2_EMPTY"):  # A/B: return torch's cached blocks first
-            import gc
-            if args.rollout_T > 0:
-                del module
-            gc.collect()
-            torch.cuda.empty_cache()
         c2 = c2_line(args, rank)
     tt = torch.tensor([dt, t_roll], dtype=torch.float64, device="cuda")
     if world > 1:
