@@ -608,7 +608,10 @@ __global__ __launch_bounds__(BS * (1 + G)) void demand_park4_kernel(const DevEnv
 constexpr int UD = MSC_UD;                  // uniforms per round
 constexpr int UHS = MSC_UHS;                // rounds per chunk (<= UD * UHS draws per lane)
 constexpr int pow2ceil(int x) { return x <= 1 ? 1 : 2 * pow2ceil((x + 1) / 2); }
-constexpr int UCAP = pow2ceil(2 * UD * UHS);  // ring capacity (positions), >= 2 chunks
+#ifndef MSC_UCAP_X
+#define MSC_UCAP_X 1  // A/B: ring capacity multiplier (deeper rings, fewer demand blocks per CU)
+#endif
+constexpr int UCAP = pow2ceil(2 * UD * UHS) * MSC_UCAP_X;  // ring capacity (positions), >= 2 chunks
 constexpr int USLOTS = UCAP + UD;           // ring rows: UCAP + the UD - 1 mirrored ones + a dummy row
 static_assert((UCAP & (UCAP - 1)) == 0, "ring layout");
 

@@ -231,6 +231,7 @@ class _Lane:
     def __init__(self, env: VecInventoryEnv, e0: int, stream: Optional[torch.cuda.Stream], flat: Optional[torch.Tensor]):
         self.env, self.e0, self.e1, self.stream, self.flat = env, e0, e0 + env.n_envs, stream, flat
         self.noise: Optional[torch.Tensor] = None
+        self.critic_stream: Optional[torch.cuda.Stream] = None  # V(obs_t) off the step chain
         self.obs_filtered = False  # the env's current observation already went through the obs filter
 
     def ctx(self):
@@ -271,6 +272,7 @@ class RolloutCollector:
         self.next_values = torch.zeros((T, E, W), device=dev)
         self.terminated = torch.zeros((T, E, W), dtype=torch.uint8, device=dev)
         self.truncated = torch.zeros((T, E, W), dtype=torch.uint8, device=dev)
+        self._trunc_env = torch.zeros((T, E), dtype=torch.uint8, device=dev)  # the env writes these rows
         self.adv = torch.empty((T, E, W), device=dev)
         self.targets = torch.empty((T, E, W), device=dev)
         if adv_groups not in (1, W):
@@ -278,6 +280,13 @@ class RolloutCollector:
         self.adv_groups = int(adv_groups)
         self.stats = torch.zeros((self.adv_groups, 3), dtype=torch.float64, device=dev)
         self._need_flat = module.rc.actor_obs_type == "global"  # the critic splits its first layer
+        # The values of obs_t are read only by the GAE after the rollout: with few envs the critic runs
+        # on a side stream per lane, after the step that wrote obs_t, beside the actor -> sampling ->
+        # env chain (C2 IPPO rollout 136.9 -> 139.5 M agent-steps/s); on a full chip it only takes
+        # issue slots from the env kernels (C3 MAPPO 224.7 -> 214.9 M), and not when it reads the
+        # lane's flat buffer, which the next step rewrites. MSC_ROLLOUT_CRITIC_SIDE=0|1 forces it.
+        cs = os.environ.get("MSC_ROLLOUT_CRITIC_SIDE")
+        self._critic_side = (self.N <= 65536 if cs is None else cs != "0") and not self._need_flat
         self._gen = torch.Generator(device=dev).manual_seed(seed)
         # obs_normalization "meanstd": RLlib's running filter, one per lane (env runner), synchronised
         # after every collect (marlsc/obs_filter.py)
@@ -301,8 +310,17 @@ class RolloutCollector:
         env, m, sl = ln.env, self.module, slice(ln.e0, ln.e1)
         obs = self._obs_all[t, sl]
         full = self._full(ln, obs)
+        if self._critic_side:
+            if ln.critic_stream is None:
+                ln.critic_stream = torch.cuda.Stream(device=obs.device)
+            ev = torch.cuda.Event()
+            ev.record()
+            ln.critic_stream.wait_event(ev)
+            with torch.cuda.stream(ln.critic_stream):
+                self.values[t, sl] = m.values(obs, full)
         mean, log_std = m.dist_inputs(obs, full)
-        self.values[t, sl] = m.values(obs, full)
+        if not self._critic_side:
+            self.values[t, sl] = m.values(obs, full)
         # standard-normal noise for NOISE_CHUNK steps of the lane at once (one launch instead of one
         # per step)
         if t % NOISE_CHUNK == 0:
@@ -313,13 +331,13 @@ class RolloutCollector:
         # log_std [E, W, K] is a broadcast of one row (shared policy) or of W rows (per agent)
         a = gaussian_sample(mean.contiguous(), log_std[0], m.rc.logstd_floor, eps, self.actions[t, sl], self.logp[t, sl])
         may_end = env.may_truncate()
-        _, _, trunc, final_obs = env.step(a, obs_out=self._obs_all[t + 1, sl], rewards_out=self.rewards[t, sl])
+        _, _, trunc, final_obs = env.step(a, obs_out=self._obs_all[t + 1, sl], rewards_out=self.rewards[t, sl],
+                                          truncated_out=self._trunc_env[t, sl])
         li = self._lanes.index(ln) if self.obs_filter is not None else 0
         if self.obs_filter is not None:  # the new observations first, then the truncated envs' final ones
             self.obs_filter.apply(li, self._obs_all[t + 1, sl])
             if may_end:
                 self.obs_filter.apply(li, final_obs, mask=trunc)
-        self.truncated[t, sl] = trunc.unsqueeze(-1)
         # truncation bootstrap: V(final_obs) for the envs whose episode ended at this step
         # (skipped while the envs are known to be mid-episode in lockstep; next_values is zeroed
         # once per rollout)
@@ -358,6 +376,10 @@ class RolloutCollector:
                 ln.env.obs.copy_(last)  # the env's own buffer holds the current observation again
             if ln.stream is not None:
                 main.wait_stream(ln.stream)
+            if ln.critic_stream is not None:
+                main.wait_stream(ln.critic_stream)
+        # the per-env truncation flags of every step to every agent's sequence (one launch)
+        self.truncated.copy_(self._trunc_env.unsqueeze(-1).expand_as(self.truncated))
         if self.obs_filter is not None:
             self.obs_filter.sync()
         N = self.N

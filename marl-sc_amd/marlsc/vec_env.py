@@ -98,16 +98,20 @@ class VecInventoryEnv:
 
     def step(self, actions: torch.Tensor, *, want_final_obs: bool = True, want_f64: bool = False,
              info: Optional[Dict[str, torch.Tensor]] = None, obs_out: Optional[torch.Tensor] = None,
-             rewards_out: Optional[torch.Tensor] = None):
+             rewards_out: Optional[torch.Tensor] = None, truncated_out: Optional[torch.Tensor] = None):
         """actions [E, W, K] float32 on the device. Returns (obs [E,W,L], rewards [E,W],
         truncated [E] bool-as-u8, final_obs [E,W,L] or None). Returned tensors are internal
         buffers, overwritten by the next call. obs_out / rewards_out (contiguous f32 [E,W,L] / [E,W]
         on the device, e.g. a rollout buffer's row): written instead of the internal buffers, which
-        then keep their previous contents (`obs` is stale until the caller copies the latest back)."""
+        then keep their previous contents (`obs` is stale until the caller copies the latest back).
+        truncated_out (contiguous uint8 [E] on the device): the truncation flags, likewise."""
         for name, t, shape in (("obs_out", obs_out, (self.n_envs, self.W, self.L)), ("rewards_out", rewards_out, (self.n_envs, self.W))):
             if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device
                                   or tuple(t.shape) != shape):
                 raise ValueError(f"{name} must be a contiguous float32 {shape} tensor on {self.device}")
+        if truncated_out is not None and (truncated_out.dtype != torch.uint8 or not truncated_out.is_contiguous()
+                                          or truncated_out.device != self.device or tuple(truncated_out.shape) != (self.n_envs,)):
+            raise ValueError(f"truncated_out must be a contiguous uint8 ({self.n_envs},) tensor on {self.device}")
         if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
             actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
         if actions.shape != (self.n_envs, self.W, self.K):
@@ -120,12 +124,13 @@ class VecInventoryEnv:
             si = C.byref(s)
         obs = self.obs if obs_out is None else obs_out
         rew = self.rewards if rewards_out is None else rewards_out
+        tr = self.truncated if truncated_out is None else truncated_out
         abi.check(abi.lib().msc_env_step(
             self._h, _p(actions), _p(obs), _p(rew), _p(self.rewards_f64) if want_f64 else None,
-            _p(self.truncated), _p(self.final_obs) if want_final_obs else None, si, _stream()))
+            _p(tr), _p(self.final_obs) if want_final_obs else None, si, _stream()))
         ts = getattr(self, "_t_sync", -1)
         self._t_sync = -1 if ts < 0 else (0 if ts + 1 >= self.spec.episode_length else ts + 1)
-        return obs, rew, self.truncated, (self.final_obs if want_final_obs else None)
+        return obs, rew, tr, (self.final_obs if want_final_obs else None)
 
     def may_truncate(self) -> bool:
         """Whether the next step() can end an episode (host-side lockstep tracking, no sync): False
