@@ -33,7 +33,7 @@ namespace msc {
 #endif
 constexpr int AL_CH = MSC_AL_CH;
 template <int K>
-void launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
+hipError_t launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
 #ifndef MSC_AL_PRIO
 #define MSC_AL_PRIO 3  // s_setprio: the step chain is the critical path next to the demand waves
 #endif
@@ -477,15 +477,15 @@ static bool alloc_tab_in_lds(const EnvConst& c, int MW, int LPE) {
          alloc_lane_lds_bytes(c, MW, LPE, true) <= 160 * 1024;
 }
 template <typename F>
-static void alloc_launch(F f, const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st, int lpe, size_t lds) {
-  if (lds > 64 * 1024) {  // above the default dynamic LDS limit (gfx950: 160 KiB per workgroup)
-    static thread_local const void* done = nullptr;  // the kernel configured last
-    if (done != (const void*)f) {
-      (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      done = (const void*)f;
-    }
+static hipError_t alloc_launch(F f, const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st, int lpe,
+                               size_t lds) {
+  if (lds > 64 * 1024) {  // above the default dynamic LDS limit (gfx950: 160 KiB per workgroup); set
+                          // on every such launch: the attribute is per function and device
+    const hipError_t e = hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(f, dim3((unsigned)((c.E * lpe + 63) / 64)), dim3(64), lds, st, d, io);
+  return hipGetLastError();
 }
 
 // lanes per env: 1 unless MSC_ALLOC_LPE asks for 2 or 4 (measured slower at every BASELINE shape:
@@ -499,7 +499,7 @@ static int alloc_lpe(const EnvConst& c, bool dbg, int MW) {
 }
 
 template <int K, int MW, bool EXACT>
-void launch_alloc_mw(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
+hipError_t launch_alloc_mw(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   using KFn = void (*)(const DevEnv*, StepIO);
   const bool dbg = io.has_info != 0;
   const int lpe = alloc_lpe(c, dbg, MW);
@@ -511,8 +511,7 @@ void launch_alloc_mw(const EnvConst& c, const DevEnv* d, const StepIO& io, hipSt
     if (lpe > 1) {
       f = lpe == 4 ? (tab ? MSC_AL(false, true, false, 4) : MSC_AL(false, false, false, 4))
                    : (tab ? MSC_AL(false, true, false, 2) : MSC_AL(false, false, false, 2));
-      alloc_launch(f, c, d, io, st, lpe, lds);
-      return;
+      return alloc_launch(f, c, d, io, st, lpe, lds);
     }
   }
   if (shared_homes(c))
@@ -522,25 +521,19 @@ void launch_alloc_mw(const EnvConst& c, const DevEnv* d, const StepIO& io, hipSt
     f = dbg ? (tab ? MSC_AL(true, true, false, 1) : MSC_AL(true, false, false, 1))
             : (tab ? MSC_AL(false, true, false, 1) : MSC_AL(false, false, false, 1));
 #undef MSC_AL
-  alloc_launch(f, c, d, io, st, 1, lds);
+  return alloc_launch(f, c, d, io, st, 1, lds);
 }
 
 template <int K>
-void launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
+hipError_t launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   // exact instantiations for the warehouse counts of the BASELINE configs (2, 8, 16), masked ones
   // (next power of two) otherwise
-  if (c.W == 2)
-    launch_alloc_mw<K, 2, true>(c, d, io, st);
-  else if (c.W <= 4)
-    launch_alloc_mw<K, 4, false>(c, d, io, st);
-  else if (c.W == 8)
-    launch_alloc_mw<K, 8, true>(c, d, io, st);
-  else if (c.W < 8)
-    launch_alloc_mw<K, 8, false>(c, d, io, st);
-  else if (c.W == 16)
-    launch_alloc_mw<K, 16, true>(c, d, io, st);
-  else
-    launch_alloc_mw<K, 16, false>(c, d, io, st);
+  if (c.W == 2) return launch_alloc_mw<K, 2, true>(c, d, io, st);
+  if (c.W <= 4) return launch_alloc_mw<K, 4, false>(c, d, io, st);
+  if (c.W == 8) return launch_alloc_mw<K, 8, true>(c, d, io, st);
+  if (c.W < 8) return launch_alloc_mw<K, 8, false>(c, d, io, st);
+  if (c.W == 16) return launch_alloc_mw<K, 16, true>(c, d, io, st);
+  return launch_alloc_mw<K, 16, false>(c, d, io, st);
 }
 
 // The kernels are instantiated in sixteen translation units so the build runs them in parallel:
@@ -550,10 +543,10 @@ void launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO& io, h
 #ifndef MSC_AL_PART
 #define MSC_AL_PART 0
 #endif
-#define MSC_AL_MW(KV, MWV, EX, KW) KW template void launch_alloc_mw<KV, MWV, EX>(const EnvConst&, const DevEnv*, const StepIO&, hipStream_t);
+#define MSC_AL_MW(KV, MWV, EX, KW) KW template hipError_t launch_alloc_mw<KV, MWV, EX>(const EnvConst&, const DevEnv*, const StepIO&, hipStream_t);
 #define MSC_AL_EXACT(KV, KW) MSC_AL_MW(KV, 2, true, KW) MSC_AL_MW(KV, 8, true, KW) MSC_AL_MW(KV, 16, true, KW)
 #define MSC_AL_MASKED(KV, KW) MSC_AL_MW(KV, 4, false, KW) MSC_AL_MW(KV, 8, false, KW) MSC_AL_MW(KV, 16, false, KW)
-#define MSC_AL_K(KV) template void launch_alloc_lane_k<KV>(const EnvConst&, const DevEnv*, const StepIO&, hipStream_t);
+#define MSC_AL_K(KV) template hipError_t launch_alloc_lane_k<KV>(const EnvConst&, const DevEnv*, const StepIO&, hipStream_t);
 #if MSC_AL_PART == 0
 #define MSC_AL_ALL(KV) MSC_AL_EXACT(KV, ) MSC_AL_MASKED(KV, ) MSC_AL_K(KV)
 MSC_AL_ALL(1) MSC_AL_ALL(2) MSC_AL_ALL(3) MSC_AL_ALL(4) MSC_AL_ALL(5) MSC_AL_ALL(6) MSC_AL_ALL(7) MSC_AL_ALL(8)
@@ -578,17 +571,16 @@ MSC_AL_MASKED(MSC_AL_PART / 2, )
 #if MSC_AL_PART == 0 || MSC_AL_PART == 1
 hipError_t launch_alloc_lane(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   switch (c.K) {
-    case 1: launch_alloc_lane_k<1>(c, d, io, st); break;
-    case 2: launch_alloc_lane_k<2>(c, d, io, st); break;
-    case 3: launch_alloc_lane_k<3>(c, d, io, st); break;
-    case 4: launch_alloc_lane_k<4>(c, d, io, st); break;
-    case 5: launch_alloc_lane_k<5>(c, d, io, st); break;
-    case 6: launch_alloc_lane_k<6>(c, d, io, st); break;
-    case 7: launch_alloc_lane_k<7>(c, d, io, st); break;
-    case 8: launch_alloc_lane_k<8>(c, d, io, st); break;
+    case 1: return launch_alloc_lane_k<1>(c, d, io, st);
+    case 2: return launch_alloc_lane_k<2>(c, d, io, st);
+    case 3: return launch_alloc_lane_k<3>(c, d, io, st);
+    case 4: return launch_alloc_lane_k<4>(c, d, io, st);
+    case 5: return launch_alloc_lane_k<5>(c, d, io, st);
+    case 6: return launch_alloc_lane_k<6>(c, d, io, st);
+    case 7: return launch_alloc_lane_k<7>(c, d, io, st);
+    case 8: return launch_alloc_lane_k<8>(c, d, io, st);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 #endif
 

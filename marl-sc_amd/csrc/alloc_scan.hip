@@ -486,7 +486,7 @@ size_t alloc_scan_lds_bytes(const EnvConst& c) {
 bool alloc_scan_supported(int W, int K) { return W <= 8 && K <= 6; }
 
 template <int K>
-static void launch_scan_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
+static hipError_t launch_scan_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   using KFn = void (*)(const DevEnv*, StepIO);
   const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : 8;
   const bool t = alloc_scan_tab(c, GW);
@@ -494,22 +494,25 @@ static void launch_scan_k(const EnvConst& c, const DevEnv* d, const StepIO& io, 
         : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true> : (KFn)alloc_scan_kernel<K, 4, false>)
                   : (t ? (KFn)alloc_scan_kernel<K, 8, true> : (KFn)alloc_scan_kernel<K, 8, false>);
   const size_t lds = alloc_scan_lds_bytes(c);
-  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(f, dim3((unsigned)((c.E + SC_WAVES - 1) / SC_WAVES)), dim3(64 * SC_WAVES), lds, st, d, io);
+  return hipGetLastError();
 }
 
 hipError_t launch_alloc_scan(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   if (!alloc_scan_supported(c.W, c.K)) return hipErrorInvalidValue;
   switch (c.K) {
-    case 1: launch_scan_k<1>(c, d, io, st); break;
-    case 2: launch_scan_k<2>(c, d, io, st); break;
-    case 3: launch_scan_k<3>(c, d, io, st); break;
-    case 4: launch_scan_k<4>(c, d, io, st); break;
-    case 5: launch_scan_k<5>(c, d, io, st); break;
-    case 6: launch_scan_k<6>(c, d, io, st); break;
+    case 1: return launch_scan_k<1>(c, d, io, st);
+    case 2: return launch_scan_k<2>(c, d, io, st);
+    case 3: return launch_scan_k<3>(c, d, io, st);
+    case 4: return launch_scan_k<4>(c, d, io, st);
+    case 5: return launch_scan_k<5>(c, d, io, st);
+    case 6: return launch_scan_k<6>(c, d, io, st);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 #ifdef MSC_PROF
