@@ -446,17 +446,21 @@ def compute_obs_statistics(env_config: Any, seed_manager, mode: str = "meanstd_c
     spec = EnvSpec.from_config(env_config, meta)
     env = VecInventoryEnv(None, 1, spec=spec, device=device, env_seeds=np.array([env_seed], dtype=np.uint32))
     rng = np.random.default_rng(action_seed)
-    W, K, T = spec.W, spec.K, spec.episode_length
-    samples = []
+    W, K, T, L = spec.W, spec.K, spec.episode_length, spec.n_features
+    # samples stay on the device, [episode][step 0..T][agent][L] (agent order, the terminal observation
+    # of each episode last), and come to the host once; no host round trip per step
+    samples = torch.empty((n_episodes, T + 1, W, L), dtype=torch.float32, device=env.device)
     obs = env.reset()
-    for _ in range(n_episodes):
+    for ep in range(n_episodes):
+        # one episode's actions in one draw: rng.uniform(size=(T, W, K)) is the same stream as the
+        # reference's per-step, per-agent uniform(size=(K,)) calls, in the same order
+        acts = torch.from_numpy(rng.uniform(-1, 1, size=(T, W, K)).astype(np.float32)).to(env.device)
         for t in range(T):
-            samples.append(obs[0].cpu().numpy())
-            a = np.stack([rng.uniform(-1, 1, size=(K,)).astype(np.float32) for _ in range(W)])
-            obs, _, trunc, final = env.step(torch.from_numpy(a).to(env.device).unsqueeze(0))
-        samples.append(final[0].cpu().numpy())  # the terminal observation of the episode
+            samples[ep, t].copy_(obs[0])
+            obs, _, trunc, final = env.step(acts[t].unsqueeze(0))
+        samples[ep, T].copy_(final[0])
+    all_obs = samples.reshape(-1, L).cpu().numpy()  # [(T + 1) * n_episodes * W, L]
     env.close()
-    all_obs = np.concatenate(samples, axis=0)  # [(T + 1) * n_episodes * W, L] in agent order
     return obs_statistics_from_samples(all_obs, mode, spec)
 
 

@@ -61,6 +61,24 @@ def pack_demand_trace(src: Any, n_skus: int, data_mode: str = "train") -> Dict[s
             "regions": regions, "quantities": quant.astype(np.int32)}
 
 
+def _group_mean(vals) -> float:
+    """The f64 mean pandas' `groupby(...).mean()` computes for one group (its cython group_mean):
+    a Kahan-compensated running sum in row order, NaNs skipped, divided by the count. A plain
+    sum / len can differ in the last ulp and flip `idxmin` between near-equal regions."""
+    total, comp, n = 0.0, 0.0, 0
+    for v in vals:
+        if v != v:
+            continue
+        n += 1
+        y = v - comp
+        t = total + y
+        comp = t - total - y
+        if comp != comp:
+            comp = 0.0
+        total = t
+    return total / n if n else float("nan")
+
+
 def map_excluded_regions(order_region_ids, selected_region_ids, warehouse_to_region) -> "np.ndarray":
     """`DataProcessor.map_excluded_regions` (src/data/preprocessor.py:382-441), restated on numpy
     columns: an order whose region is not selected moves to the selected region that shares
@@ -99,7 +117,10 @@ def map_excluded_regions(order_region_ids, selected_region_ids, warehouse_to_reg
                 groups = {}
                 for k, v in zip(keys.tolist(), costs.tolist()):
                     groups.setdefault(k, []).append(v)
-                best_k = min(sorted(groups), key=lambda k: sum(groups[k]) / len(groups[k]))
+                means = {k: _group_mean(v) for k, v in groups.items()}
+                # idxmin: NaN means skipped, the first minimum in sorted key order
+                cand = [k for k in sorted(groups) if means[k] == means[k]] or sorted(groups)
+                best_k = min(cand, key=lambda k: means[k])
                 nearest = next((r for r in sel if str(r) == str(best_k)), sel[0])
         out[ids_str == ex_s] = nearest
     return out

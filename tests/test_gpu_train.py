@@ -22,11 +22,17 @@ def _algo(name, **over):
     return PPOConfig.from_algorithm_config(raw)
 
 
+def cfg_features(cfg):
+    from marlsc.spec import EnvSpec
+    return dict(EnvSpec.from_config(cfg, {}).features)
+
+
 @pytest.mark.parametrize("mode", ["meanstd_custom", "meanstd_grouped"])
 def test_obs_statistics_gpu_equal_oracle_episodes(mode):
     import oracle as orc
     from marlsc import SeedManager, make_synthetic_env_config
-    from marlsc.ppo import compute_obs_statistics, obs_statistics_from_samples
+    from obs_stats_ref import obs_statistics_ref
+    from marlsc.ppo import compute_obs_statistics
     from marlsc.spec import EnvSpec
     cfg = make_synthetic_env_config(3, 5, 2, episode_length=12)
     sm = SeedManager(2024)
@@ -45,7 +51,8 @@ def test_obs_statistics_gpu_equal_oracle_episodes(mode):
             a = np.stack([rng.uniform(-1, 1, size=(spec.K,)).astype(np.float32) for _ in range(spec.W)])
             obs, _, _, fo = env.step(a[None], final_obs=True)
         samples.append(fo[0])
-    m2, s2 = obs_statistics_from_samples(np.concatenate(samples), mode, spec)
+    # the statistics by the oracle's restatement of obs_stats.py (groups from the feature flags)
+    m2, s2 = obs_statistics_ref(np.concatenate(samples), mode, cfg_features(cfg), spec.K, spec.max_expected_lead_time)
     np.testing.assert_array_equal(mean, m2)
     np.testing.assert_array_equal(std, s2)
 

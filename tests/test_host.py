@@ -353,3 +353,39 @@ def test_checkpoint_bookkeeping_of_the_reference_runner(tmp_path):
     assert [x["iteration"] for x in kept] == [1, 2, 3] and best == -3.0 and best_it == 2
     kept, best, best_it = load_and_truncate_training_metrics(tmp_path / "nowhere", 3)
     assert kept == [] and best == float("-inf") and best_it is None
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_map_excluded_regions_vs_pandas(seed):
+    # marlsc.trace.map_excluded_regions against oracle/preproc_ref.py, which runs the reference's
+    # own pandas operations (preprocessor.py:382-441: groupby mean = Kahan-compensated sums, idxmin
+    # = first minimum in sorted key order). Costs are drawn from decimals whose group means tie or
+    # differ by an ulp between a plain sum / len and pandas' compensated sum.
+    import pandas as pd
+    from preproc_ref import map_excluded_regions_pd
+    from marlsc.trace import map_excluded_regions
+    rng = np.random.default_rng(seed)
+    regions = [f"R{i}" for i in range(40)] if seed % 2 else list(range(100, 140))
+    sel = list(rng.choice(np.array(regions, dtype=object), 15, replace=False))
+    whs = [f"W{i}" for i in range(8)]
+    n = 300
+    vals = np.array([0.1, 0.2, 0.3, 0.7, 1.1, 1e16, -1e16, 3.0, 0.30000000000000004])
+    w2r = pd.DataFrame({"sourcenodeid": rng.choice(whs, n),
+                        "destinationregionid": [regions[i] for i in rng.integers(0, 40, n)],
+                        "fixed_costs": rng.choice(vals[:5] if seed < 3 else vals, n)})
+    w2r = w2r[~w2r["destinationregionid"].isin(regions[35:])]  # some excluded regions have no pairs
+    orders = np.array([regions[i] for i in rng.integers(0, 40, 2000)], dtype=object)
+    got = map_excluded_regions(orders, sel, {c: w2r[c].tolist() for c in w2r.columns})
+    want = map_excluded_regions_pd(orders, sel, w2r.reset_index(drop=True))
+    assert got.tolist() == want.tolist()
+
+
+def test_group_mean_is_pandas_groupby_mean():
+    import pandas as pd
+    from marlsc.trace import _group_mean
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        v = rng.choice([0.1, 0.2, 0.3, 0.7, 1e16, -1e16, 2.5e-3, np.nan], rng.integers(1, 30))
+        want = pd.DataFrame({"k": 0, "v": v}).groupby("k")["v"].mean().iloc[0]
+        got = _group_mean(v.tolist())
+        assert (got == want) or (got != got and want != want), (v, got, want)

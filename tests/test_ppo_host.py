@@ -174,6 +174,41 @@ def test_grouped_observation_statistics_arithmetic():
     assert np.all(mg[p0:p0 + lt * K] == np.float32(float(x[:, p0:p0 + lt * K].mean())))
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_observation_statistics_vs_oracle_restatement(seed):
+    # the product's statistics (marlsc/ppo.py: feature_groups + obs_statistics_from_samples) against
+    # the oracle's restatement of obs_stats.py:73-169 over random feature sets (every group, with and
+    # without aggregates), bit-exact: both run the reference's numpy calls on the same f32 samples
+    from obs_stats_ref import obs_statistics_ref
+    from marlsc.ppo import obs_statistics_from_samples
+    from marlsc import make_synthetic_env_config
+    from marlsc.spec import EnvSpec
+    from marlsc.synthetic import FEATURE_CONFIG_YAML
+    rng = np.random.default_rng(seed)
+    names = ["inventory", "pipeline", "incoming_demand_home", "units_shipped_home", "units_shipped_away",
+             "stockout", "rolling_demand_mean", "demand_forecast"]
+    aggs = ["inventory_aggregate", "pipeline_aggregate", "incoming_demand_home_aggregate",
+            "units_shipped_away_aggregate", "rolling_demand_mean_aggregate", "demand_forecast_aggregate"]
+    feats = {**FEATURE_CONFIG_YAML, **{k: bool(rng.integers(0, 2)) for k in names + aggs}}
+    feats["inventory"] = feats["pipeline"] = True  # always on (schema validator)
+    for parent, agg in [("inventory", "inventory_aggregate"), ("pipeline", "pipeline_aggregate"),
+                        ("incoming_demand_home", "incoming_demand_home_aggregate"),
+                        ("units_shipped_away", "units_shipped_away_aggregate"),
+                        ("rolling_demand_mean", "rolling_demand_mean_aggregate"),
+                        ("demand_forecast", "demand_forecast_aggregate")]:
+        feats[agg] = feats[agg] and feats[parent]
+    cfg = make_synthetic_env_config(3, 4, 1 + seed % 3, episode_length=6, features=feats)
+    spec = EnvSpec.from_config(cfg, {})
+    x = rng.normal(rng.uniform(-5, 5, spec.n_features), rng.uniform(0.1, 3, spec.n_features),
+                   size=(257, spec.n_features)).astype(np.float32)
+    x[:, rng.integers(0, spec.n_features)] = 2.5  # a constant column: std 1.0
+    for mode in ("meanstd_custom", "meanstd_grouped"):
+        m, s = obs_statistics_from_samples(x, mode, spec)
+        m2, s2 = obs_statistics_ref(x, mode, dict(spec.features), spec.K, spec.max_expected_lead_time)
+        np.testing.assert_array_equal(m, m2)
+        np.testing.assert_array_equal(s, s2)
+
+
 def _grad_worker(rank, world, port, out):
     import torch.distributed as dist
     from marlsc.ppo import allreduce_grads
