@@ -337,6 +337,31 @@ int msc_mlp2_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_
                           const float* w1p, const float* b1, const float* w3p, const float* b3, float* out,
                           const float* pre1, int32_t pre1_group, msc_stream_t stream);
 
+/* The actor forward and the rollout's action sampling in one launch: msc_mlp3_relu_forward /
+ * msc_mlp2_relu_forward followed, while the out_dim means of each row are still in registers, by
+ * msc_gaussian_sample's arithmetic (bit-identical to the separate call) into sample->actions /
+ * logp / clipped. out (the means) may be NULL. Needs the VALU output layer (out_dim <= 8,
+ * msc_mlp3_w3_layout(out_dim) == 1). Replaces the EnvRunner's _forward_inference -> TorchDiagGaussian
+ * sample pair (rlmodules/base.py:480-557). */
+typedef struct msc_gaussian_epilogue {
+  const float* log_std;   /* [log_std_rows][out_dim]: row n % log_std_rows applies to row n */
+  int32_t log_std_rows;
+  float logstd_floor;
+  const float* eps;       /* [n_rows][out_dim] standard-normal draws */
+  float* actions;         /* [n_rows][out_dim] */
+  float* logp;            /* [n_rows] */
+  float* clipped;         /* [n_rows][out_dim] */
+} msc_gaussian_epilogue;
+int msc_mlp3_relu_forward_sampled(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
+                                  int32_t out_dim, const float* w1p, const float* b1, const float* w2p,
+                                  const float* b2, const float* w3p, const float* b3, float* out,
+                                  const float* pre1, int32_t pre1_group, const msc_gaussian_epilogue* sample,
+                                  msc_stream_t stream);
+int msc_mlp2_relu_forward_sampled(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden, int32_t out_dim,
+                                  const float* w1p, const float* b1, const float* w3p, const float* b3, float* out,
+                                  const float* pre1, int32_t pre1_group, const msc_gaussian_epilogue* sample,
+                                  msc_stream_t stream);
+
 /* Utility: SeedSequence(words).generate_state(1, uint32)[0] (numpy-compatible), on the host. */
 uint32_t msc_seedseq_u32(const uint32_t* words, int32_t n_words);
 

@@ -399,6 +399,12 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     // step_c observation staging when the block's stage fits (C3: 8 x 64 x 35 floats = 70 KiB)
     c.obs_stage = (size_t)BS * ((c.W * c.L) | 1) * sizeof(float) <= 80 * 1024 ? 1 : 0;
     if (const char* os = getenv("MSC_OBS_STAGE")) c.obs_stage = c.obs_stage && atoi(os) != 0;
+    // step_c with the pending ring in registers (8-wave blocks, up to 256 VGPRs): C2 (4,096 envs)
+    // 152.7 -> 157.4 M agent-steps/s; at 32,768 envs the env line is unchanged and the MAPPO rollout
+    // 1.165 -> 1.188 ms per step (fewer step_c blocks fit beside the demand kernel), so only below
+    // the lane allocator's env count (profiles/r03/ab_ringreg.txt). MSC_OBS_RING_REG=0|1 forces it.
+    c.obs_ring_reg = n_envs < 16384 ? 1 : 0;
+    if (const char* orr = getenv("MSC_OBS_RING_REG")) c.obs_ring_reg = atoi(orr) != 0;
     // phase B: one env per lane (alloc_lane_kernel) when there are enough env chains to fill the
     // chip and the Poisson demand kernel of the next step runs beside it (it then needs the issue
     // slots the lane kernel leaves free: C3, 32768 envs: 0.80 vs 0.86 ms/step); otherwise the
@@ -1098,38 +1104,86 @@ int msc_meanstd_filter(const float* obs, float* out, int64_t n_rows, int32_t n_c
 
 int msc_mlp3_w3_layout(int32_t out_dim) { return out_dim >= 1 && out_dim <= 32 ? (mlp3_valu_outputs(out_dim) > 0 ? 1 : 0) : -1; }
 
-int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
-                          int32_t out_dim, const float* w1p, const float* b1, const float* w2p, const float* b2,
-                          const float* w3p, const float* b3, float* out, const float* pre1, int32_t pre1_group,
-                          msc_stream_t stream) {
+static int mlp_sample_args(const msc_gaussian_epilogue* g, int out_dim, MlpSample* sm) {
+  if (!g) return 0;
+  if (!g->log_std || !g->eps || !g->actions || !g->logp || !g->clipped) return set_err(-1, "null sampling buffer");
+  if (g->log_std_rows < 1) return set_err(-1, "log_std_rows %d must be >= 1", g->log_std_rows);
+  if (mlp3_valu_outputs(out_dim) == 0)
+    return set_err(-1, "sampling epilogue needs the VALU output layer (out_dim %d <= 8)", out_dim);
+  *sm = MlpSample{g->log_std, g->log_std_rows, g->logstd_floor, g->eps, g->actions, g->logp, g->clipped};
+  return 0;
+}
+
+static int mlp3_impl(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2, int32_t out_dim,
+                     const float* w1p, const float* b1, const float* w2p, const float* b2, const float* w3p,
+                     const float* b3, float* out, const float* pre1, int32_t pre1_group,
+                     const msc_gaussian_epilogue* sample, msc_stream_t stream) {
   if (pre1 && pre1_group < 1) return set_err(-1, "pre1_group %d must be >= 1", pre1_group);
   // the kernel reads b1 / b2 / pre1 rows as float4
   if (((uintptr_t)b1 | (uintptr_t)b2 | (uintptr_t)pre1 | (uintptr_t)w1p | (uintptr_t)w2p | (uintptr_t)w3p) & 15)
     return set_err(-1, "b1, b2, pre1 and the packed weights must be 16-byte aligned");
-  if (!x || !w1p || !b1 || !w2p || !b2 || !w3p || !b3 || !out) return set_err(-1, "null argument");
+  if (!x || !w1p || !b1 || !w2p || !b2 || !w3p || !b3 || (!out && !sample)) return set_err(-1, "null argument");
   if (n_rows < 0 || in_dim < 1 || in_dim > 1024 || out_dim < 1 || out_dim > 32)
     return set_err(-1, "bad shape (n_rows %lld, in_dim %d, out_dim %d)", (long long)n_rows, in_dim, out_dim);
   auto hs = [](int h) { return h == 64 || h == 128 || h == 256 || h == 512; };
   if (!(hs(hidden1) && hs(hidden2)))
     return set_err(-1, "hidden sizes %d, %d: the fused MLP supports [H1, H2] with H1, H2 in {64, 128, 256, 512}", hidden1, hidden2);
+  MlpSample sm{};
+  if (const int r = mlp_sample_args(sample, out_dim, &sm)) return r;
   HIP_TRY(launch_mlp3_relu(x, n_rows, in_dim, hidden1, hidden2, out_dim, w1p, b1, w2p, b2, w3p, b3, out, pre1,
-                           pre1 ? pre1_group : 1, (hipStream_t)stream));
+                           pre1 ? pre1_group : 1, (hipStream_t)stream, sample ? &sm : nullptr));
+  return 0;
+}
+
+int msc_mlp3_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
+                          int32_t out_dim, const float* w1p, const float* b1, const float* w2p, const float* b2,
+                          const float* w3p, const float* b3, float* out, const float* pre1, int32_t pre1_group,
+                          msc_stream_t stream) {
+  if (!out) return set_err(-1, "null argument");
+  return mlp3_impl(x, n_rows, in_dim, hidden1, hidden2, out_dim, w1p, b1, w2p, b2, w3p, b3, out, pre1, pre1_group,
+                   nullptr, stream);
+}
+
+int msc_mlp3_relu_forward_sampled(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden1, int32_t hidden2,
+                                  int32_t out_dim, const float* w1p, const float* b1, const float* w2p,
+                                  const float* b2, const float* w3p, const float* b3, float* out,
+                                  const float* pre1, int32_t pre1_group, const msc_gaussian_epilogue* sample,
+                                  msc_stream_t stream) {
+  if (!sample) return set_err(-1, "null argument");
+  return mlp3_impl(x, n_rows, in_dim, hidden1, hidden2, out_dim, w1p, b1, w2p, b2, w3p, b3, out, pre1, pre1_group,
+                   sample, stream);
+}
+
+static int mlp2_impl(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden, int32_t out_dim, const float* w1p,
+                     const float* b1, const float* w3p, const float* b3, float* out, const float* pre1,
+                     int32_t pre1_group, const msc_gaussian_epilogue* sample, msc_stream_t stream) {
+  if (pre1 && pre1_group < 1) return set_err(-1, "pre1_group %d must be >= 1", pre1_group);
+  if (((uintptr_t)b1 | (uintptr_t)pre1 | (uintptr_t)w1p | (uintptr_t)w3p) & 15)
+    return set_err(-1, "b1, pre1 and the packed weights must be 16-byte aligned");
+  if (!x || !w1p || !b1 || !w3p || !b3 || (!out && !sample)) return set_err(-1, "null argument");
+  if (n_rows < 0 || in_dim < 1 || in_dim > 1024 || out_dim < 1 || out_dim > 32)
+    return set_err(-1, "bad shape (n_rows %lld, in_dim %d, out_dim %d)", (long long)n_rows, in_dim, out_dim);
+  if (!mlp2_supported(hidden)) return set_err(-1, "hidden size %d: the fused MLP supports multiples of 32 up to 1024", hidden);
+  MlpSample sm{};
+  if (const int r = mlp_sample_args(sample, out_dim, &sm)) return r;
+  HIP_TRY(launch_mlp2_relu(x, n_rows, in_dim, hidden, out_dim, w1p, b1, w3p, b3, out, pre1, pre1 ? pre1_group : 1,
+                           (hipStream_t)stream, sample ? &sm : nullptr));
   return 0;
 }
 
 int msc_mlp2_relu_forward(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden, int32_t out_dim,
                           const float* w1p, const float* b1, const float* w3p, const float* b3, float* out,
                           const float* pre1, int32_t pre1_group, msc_stream_t stream) {
-  if (pre1 && pre1_group < 1) return set_err(-1, "pre1_group %d must be >= 1", pre1_group);
-  if (((uintptr_t)b1 | (uintptr_t)pre1 | (uintptr_t)w1p | (uintptr_t)w3p) & 15)
-    return set_err(-1, "b1, pre1 and the packed weights must be 16-byte aligned");
-  if (!x || !w1p || !b1 || !w3p || !b3 || !out) return set_err(-1, "null argument");
-  if (n_rows < 0 || in_dim < 1 || in_dim > 1024 || out_dim < 1 || out_dim > 32)
-    return set_err(-1, "bad shape (n_rows %lld, in_dim %d, out_dim %d)", (long long)n_rows, in_dim, out_dim);
-  if (!mlp2_supported(hidden)) return set_err(-1, "hidden size %d: the fused MLP supports multiples of 32 up to 1024", hidden);
-  HIP_TRY(launch_mlp2_relu(x, n_rows, in_dim, hidden, out_dim, w1p, b1, w3p, b3, out, pre1, pre1 ? pre1_group : 1,
-                           (hipStream_t)stream));
-  return 0;
+  if (!out) return set_err(-1, "null argument");
+  return mlp2_impl(x, n_rows, in_dim, hidden, out_dim, w1p, b1, w3p, b3, out, pre1, pre1_group, nullptr, stream);
+}
+
+int msc_mlp2_relu_forward_sampled(const float* x, int64_t n_rows, int32_t in_dim, int32_t hidden, int32_t out_dim,
+                                  const float* w1p, const float* b1, const float* w3p, const float* b3, float* out,
+                                  const float* pre1, int32_t pre1_group, const msc_gaussian_epilogue* sample,
+                                  msc_stream_t stream) {
+  if (!sample) return set_err(-1, "null argument");
+  return mlp2_impl(x, n_rows, in_dim, hidden, out_dim, w1p, b1, w3p, b3, out, pre1, pre1_group, sample, stream);
 }
 
 int msc_adv_normalize_grouped(float* adv, int64_t n, int32_t n_groups, const double* stats, msc_stream_t stream) {

@@ -34,6 +34,7 @@ struct EnvConst {
   int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
   int32_t parser_rot;   // which wave of a demand block parses: (wave + rot(block)) % (1 + G) == 0 (A/B knob)
   int32_t obs_stage;    // 1: step_c stages each wave's observations in LDS and writes them coalesced
+  int32_t obs_ring_reg; // 1: step_c (<= 8 warehouses) reads the pending ring into registers before its stores
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
   int32_t shared_home;  // 1: some region is the home region of two or more warehouses
   int32_t demand_uni;   // 1: Poisson parameters equal across regions (demand_unit_kernel<UNI>)
@@ -204,11 +205,22 @@ hipError_t launch_gae(const float* r, const float* v, const float* nv, const uin
                       double* stats, hipStream_t st);
 hipError_t launch_adv_normalize(float* adv, int64_t n, int32_t n_groups, const double* stats, hipStream_t st);
 int mlp3_valu_outputs(int KO);
+// the fused MLPs' optional Gaussian-sampling epilogue (msc_gaussian_epilogue); act == nullptr: none
+struct MlpSample {
+  const float* log_std;  // [ls_rows][KO]
+  int ls_rows;
+  float floor_;
+  const float* eps;      // [n][KO]
+  float* act;            // [n][KO]
+  float* logp;           // [n]
+  float* clipped;        // [n][KO]
+};
 hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, int KO, const float* w1p, const float* b1,
                             const float* w2p, const float* b2, const float* w3p, const float* b3, float* out,
-                            const float* pre1, int grp, hipStream_t st);
+                            const float* pre1, int grp, hipStream_t st, const MlpSample* smp = nullptr);
 hipError_t launch_mlp2_relu(const float* x, int64_t n, int L, int H1, int KO, const float* w1p, const float* b1,
-                            const float* w3p, const float* b3, float* out, const float* pre1, int grp, hipStream_t st);
+                            const float* w3p, const float* b3, float* out, const float* pre1, int grp, hipStream_t st,
+                            const MlpSample* smp = nullptr);
 bool mlp2_supported(int H1);
 hipError_t launch_meanstd_filter(const float* x, float* out, int64_t E, int32_t C, const uint8_t* mask, int32_t update,
                                  double* state, double* scratch, double clip, double eps, hipStream_t st);

@@ -162,7 +162,13 @@ __device__ __noinline__ void reset_env(const EnvConst& c, const EnvState& s, int
 // ------------------------------------------------------------------------------------------
 //   shh/sht are indexed [(w * K + sku) * BS] from a pointer already offset to the env's column.
 // One agent (warehouse w) per call: the step kernel builds the W agents of an env in parallel.
-template <int K>
+#ifndef MSC_OBS_RING_REG
+#define MSC_OBS_RING_REG 4  // pending rings of up to this many slots (lead times <= 3) are read into registers
+#endif
+constexpr int OBS_RING_REG = MSC_OBS_RING_REG;
+// RREG > 0: rings of up to RREG slots are read into registers (step_c with <= 8 waves per block;
+// elsewhere the register budget is 128 and the ring is read where it is used)
+template <int K, int RREG = 0>
 __device__ __forceinline__ void build_obs_agent(const EnvConst& c, const EnvState& s, int64_t e, int w, int t_now,
                                              int n_hist, const int32_t* shh, const int32_t* sht, int64_t sstride,
                                              float* out) {
@@ -181,13 +187,16 @@ __device__ __forceinline__ void build_obs_agent(const EnvConst& c, const EnvStat
       o[(c.wid ? W : 0) + j] = x;
       j++;
     };
-    if (c.wid)
-      for (int k = 0; k < W; k++) o[k] = (k == w) ? 1.0f : 0.0f;
-    int inv[K], dh[K], sh[K], sa[K], pend_sum[K];
+    // Every state load is issued before the first observation store: vector-memory stores and loads
+    // share one completion counter (vmcnt), so a load issued after stores waits for them all; the
+    // pipeline buckets come from the pending ring held in registers (RING <= OBS_RING_REG) instead
+    // of ring reads between the feature stores.
+    int inv[K], dh[K], sh[K], sa[K], pend_sum[K], eltv[K];
     float rm[K], fc[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       const int i = w * K + sk;
+      eltv[sk] = c.elt[i];
       inv[sk] = s.inv[i * E + e];
       dh[sk] = s.inc[i * E + e];
       sh[sk] = shh ? shh[i * sstride] : 0;
@@ -201,16 +210,38 @@ __device__ __forceinline__ void build_obs_agent(const EnvConst& c, const EnvStat
     // pipeline buckets (_compute_pipeline, multi_env.py:956-966): an order of age a (ring slot
     // (t_now - a) mod RING) expects to arrive in elt - a steps and lands in bucket
     // max(1, elt - a) - 1, so bucket l >= 1 holds exactly the order of age elt - 1 - l and bucket 0
-    // every order of age >= elt - 1 (due next step or overdue). Read straight from the ring.
+    // every order of age >= elt - 1 (due next step or overdue).
+    constexpr int RR = RREG > 0 ? RREG : 1;
+    const bool ring_reg = RREG > 0 && RING <= RREG;
+    int rv[K][RR];  // ring slot q of SKU sk (ring_reg)
+    int tm = t_now % RING;
+    if (tm < 0) tm += RING;
     int pend_total = 0;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       const int32_t* rq = s.ring_q + (int64_t)(w * K + sk) * RING * E + e;
-      for (int jr = 0; jr < RING; jr++) pend_sum[sk] += rq[jr * E];
+      if (ring_reg) {
+#pragma unroll
+        for (int q = 0; q < RR; q++) rv[sk][q] = q < RING ? rq[q * E] : 0;
+#pragma unroll
+        for (int q = 0; q < RR; q++) pend_sum[sk] += rv[sk][q];
+      } else {
+        for (int jr = 0; jr < RING; jr++) pend_sum[sk] += rq[jr * E];
+      }
       pend_total += pend_sum[sk];
     }
     auto pipe_at = [&](int l, int sk) -> int {
-      const int elt = c.elt[w * K + sk];
+      const int elt = eltv[sk];
+      if (ring_reg) {  // slot q (age (tm - q) mod RING) lands in bucket max(1, elt - age) - 1
+        int v = 0;
+#pragma unroll
+        for (int q = 0; q < RR; q++) {
+          const int age = tm - q >= 0 ? tm - q : tm - q + RING;
+          const int b = elt - age > 1 ? elt - age - 1 : 0;
+          v += (q < RING && b == l) ? rv[sk][q] : 0;
+        }
+        return v;
+      }
       const int32_t* rq = s.ring_q + (int64_t)(w * K + sk) * RING * E + e;
       auto at_age = [&](int a) -> int {
         int jr = (t_now - a) % RING;
@@ -222,6 +253,8 @@ __device__ __forceinline__ void build_obs_agent(const EnvConst& c, const EnvStat
       for (int a = elt - 1 > 0 ? elt - 1 : 0; a < RING; a++) v += at_age(a);
       return v;
     };
+    if (c.wid)
+      for (int k = 0; k < W; k++) o[k] = (k == w) ? 1.0f : 0.0f;
     double inv_total = 0.0, shipped_total = 0.0, sa_total = 0.0;
     float dh_total = 0.0f;
 #pragma unroll
@@ -292,7 +325,7 @@ __device__ __forceinline__ void build_obs_agent(const EnvConst& c, const EnvStat
     if (f & MSC_F_NET_POSITION) {
 #pragma unroll
       for (int sk = 0; sk < K; sk++) {
-        double v = ((double)inv[sk] + (double)pend_sum[sk]) - (double)fc[sk] * (double)c.elt[w * K + sk];
+        double v = ((double)inv[sk] + (double)pend_sum[sk]) - (double)fc[sk] * (double)eltv[sk];
         put((double)(float)v);
       }
     }
@@ -1585,8 +1618,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
 }
 
 // ---- phase C ------------------------------------------------------------------------------
-template <int K, bool DBG>
-__global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+// WB: the most warehouses (waves) a block has; blocks of <= 8 waves get up to 256 VGPRs per lane,
+// so the observation builder holds the pending ring in registers without spilling
+template <int K, bool DBG, int WB = MSC_MAX_W>
+__global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+  constexpr int RREG = WB <= 8 ? OBS_RING_REG : 0;
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   extern __shared__ __attribute__((aligned(16))) double Lrw[];  // [W][BS] rewards (team sum)
@@ -1649,9 +1685,9 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_c_kernel(const DevEnv* __
     const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
     trunc = t + 1 >= c.T;
     if (!trunc) {
-      build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, c.obs_stage ? stg + lane * RS : io.obs + obs_off);
+      build_obs_agent<K, RREG>(c, s, e, w, t, n_hist, shh, sht, E, c.obs_stage ? stg + lane * RS : io.obs + obs_off);
     } else if (io.final_obs) {
-      build_obs_agent<K>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
+      build_obs_agent<K, RREG>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
     }
   }
   if (c.obs_stage) {
@@ -1791,7 +1827,8 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
   const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : c.W <= 8 ? 8 : 16;
   const bool dbg = io.has_info != 0;  // collect_step_info: the instrumented instantiations
   KFn a = dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>;
-  KFn cc = dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>;
+  KFn cc = (c.W <= 8 && c.obs_ring_reg) ? (dbg ? (KFn)step_c_kernel<K, true, 8> : (KFn)step_c_kernel<K, false, 8>)
+                    : (dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>);
   const bool tab = step_b_tab_bytes(c.R, c.W) <= STEP_B_TAB_MAX;
   KFn b;
 #define MSC_SB(GWV)                                                                                   \

@@ -22,11 +22,38 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "env.hpp"
+
 namespace msc {
 
 typedef float mlp_f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int mfma_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Optional epilogue: the rollout's Gaussian action sampling (msc_gaussian_sample's arithmetic,
+// operation for operation, so the results are bit-identical to the separate kernel) applied to the
+// KO outputs of row j while they are in registers: one kernel launch and the mean's HBM round trip
+// fewer per rollout step. act == nullptr: no sampling.
+template <int VKO>
+__device__ __forceinline__ void sample_row(const MlpSample& sm, int64_t j, int KO, const float (&m)[VKO]) {
+  const float half_log_2pi = 0.91893853320467274178f;  // 0.5 * log(2 pi)
+  const float* lsr = sm.log_std + (j % sm.ls_rows) * KO;
+  float lp = 0.0f;
+#pragma unroll
+  for (int a = 0; a < VKO; a++) {
+    if (a < KO) {
+      const int64_t i = j * KO + a;
+      const float ls = fmaxf(lsr[a], sm.floor_);
+      const float sd = expf(ls);
+      const float v = m[a] + sd * sm.eps[i];
+      sm.act[i] = v;
+      const float d = v - m[a];
+      lp += (-(d * d) / (2.0f * sd * sd) - ls) - half_log_2pi;
+      sm.clipped[i] = fminf(fmaxf(v, -1.0f), 1.0f);
+    }
+  }
+  sm.logp[j] = lp;
+}
 
 // NT1 / NT2: hidden tiles of 32 units; P: output tiles of layer 2 held at once (register budget:
 // 16 NT1 + 16 P + 16 accumulators + 2 x 4 P weight registers per lane).
@@ -42,7 +69,8 @@ template <int NT1, int NT2, int P, int WPE, int VKO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mlp3_relu_kernel(
     const float* __restrict__ x, int64_t n, int L, int KS1, const float4* __restrict__ w1p, const float* __restrict__ b1,
     const float4* __restrict__ w2p, const float* __restrict__ b2, const float4* __restrict__ w3p,
-    const float* __restrict__ b3, int KO, float* __restrict__ out, const float* __restrict__ pre1, int grp, int prio) {
+    const float* __restrict__ b3, int KO, float* __restrict__ out, const float* __restrict__ pre1, int grp, int prio,
+    MlpSample sm) {
   static_assert(NT2 % P == 0, "layer-2 passes");
   static_assert(VKO >= 0 && VKO <= 8, "VALU output layer: at most 8 outputs");
   constexpr int S4 = NT1 * 4;  // layer-2 k steps of 4 MFMAs (2 hidden units each)
@@ -221,11 +249,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
     for (int a = 0; a < VKO; a++) o3[a] += __shfl_xor(o3[a], 32);  // the other half's hidden units
     if (jv && h == 0) {
+      if (out) {
 #pragma unroll
-      for (int a = 0; a < VKO; a++)
-        if (a < KO) out[j * KO + a] = o3[a];
+        for (int a = 0; a < VKO; a++)
+          if (a < KO) out[j * KO + a] = o3[a];
+      }
+      if constexpr (VKO > 0) {
+        if (sm.act) sample_row<VKO>(sm, j, KO, o3);
+      }
     }
-  } else if (jv) {
+  } else if (jv && out) {  // (no sampling epilogue on the MFMA output layer: the host checks)
 #pragma unroll
     for (int r = 0; r < 16; r++) {
       const int row = mfma_row(r, h);
@@ -244,7 +277,7 @@ template <int TB, int WPE, int VKO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mlp2_relu_kernel(
     const float* __restrict__ x, int64_t n, int L, int KS1, int NT1, const float4* __restrict__ w1p,
     const float* __restrict__ b1, const float4* __restrict__ w3p, const float* __restrict__ b3, int KO,
-    float* __restrict__ out, const float* __restrict__ pre1, int grp, int prio) {
+    float* __restrict__ out, const float* __restrict__ pre1, int grp, int prio, MlpSample sm) {
   static_assert(VKO >= 0 && VKO <= 8, "VALU output layer: at most 8 outputs");
   if (prio) __builtin_amdgcn_s_setprio(3);
   const int lane = threadIdx.x & 63, h = lane >> 5;
@@ -356,11 +389,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
     for (int a = 0; a < VKO; a++) o3[a] += __shfl_xor(o3[a], 32);
     if (jv && h == 0) {
+      if (out) {
 #pragma unroll
-      for (int a = 0; a < VKO; a++)
-        if (a < KO) out[j * KO + a] = o3[a];
+        for (int a = 0; a < VKO; a++)
+          if (a < KO) out[j * KO + a] = o3[a];
+      }
+      if constexpr (VKO > 0) {
+        if (sm.act) sample_row<VKO>(sm, j, KO, o3);
+      }
     }
-  } else if (jv) {
+  } else if (jv && out) {  // (no sampling epilogue on the MFMA output layer: the host checks)
 #pragma unroll
     for (int r = 0; r < 16; r++) {
       const int row = mfma_row(r, h);
@@ -400,8 +438,10 @@ int mlp3_valu_outputs(int KO) {
 
 hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, int KO, const float* w1p, const float* b1,
                             const float* w2p, const float* b2, const float* w3p, const float* b3, float* out,
-                            const float* pre1, int grp, hipStream_t st) {
+                            const float* pre1, int grp, hipStream_t st, const MlpSample* smp) {
   if (n == 0) return hipSuccess;
+  const MlpSample sm = smp ? *smp : MlpSample{};
+  if (sm.act && mlp3_valu_outputs(KO) == 0) return hipErrorInvalidValue;  // sampling needs the VALU output layer
   const int KS1 = (L + 1) / 2;
   const int64_t tiles = (n + 31) / 32;
   const dim3 grid((unsigned)((tiles + 3) / 4)), block(256);
@@ -410,7 +450,7 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
   const float4* w3 = reinterpret_cast<const float4*>(w3p);
 #define MSC_MLP_LAUNCH(NT1, NT2, P, WPE, VKO)                                                                          \
   hipLaunchKernelGGL((mlp3_relu_kernel<NT1, NT2, P, WPE, VKO>), grid, block, 0, st, x, n, L, KS1, w1, b1, w2, b2, w3, \
-                     b3, KO, out, pre1, grp, mlp_prio())
+                     b3, KO, out, pre1, grp, mlp_prio(), sm)
   // the output layer on the VALU for KO <= 8 (VKO = 1, 2, 4, 5 or 8: the next supported count >= KO)
   const int vko = mlp3_valu_outputs(KO);
 #define MSC_MLP_VKO(NT1, NT2, P, WPE)                                 \
@@ -471,9 +511,12 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
 bool mlp2_supported(int H1) { return H1 >= 32 && H1 <= 1024 && H1 % 32 == 0; }
 
 hipError_t launch_mlp2_relu(const float* x, int64_t n, int L, int H1, int KO, const float* w1p, const float* b1,
-                            const float* w3p, const float* b3, float* out, const float* pre1, int grp, hipStream_t st) {
+                            const float* w3p, const float* b3, float* out, const float* pre1, int grp, hipStream_t st,
+                            const MlpSample* smp) {
   if (n == 0) return hipSuccess;
   if (!mlp2_supported(H1)) return hipErrorInvalidValue;
+  const MlpSample sm = smp ? *smp : MlpSample{};
+  if (sm.act && mlp3_valu_outputs(KO) == 0) return hipErrorInvalidValue;
   const int KS1 = (L + 1) / 2, NT1 = H1 / 32;
   const int TB = NT1 % 8 == 0 ? 8 : NT1 % 4 == 0 ? 4 : NT1 % 2 == 0 ? 2 : 1;
   const int64_t tiles = (n + 31) / 32;
@@ -484,7 +527,7 @@ hipError_t launch_mlp2_relu(const float* x, int64_t n, int L, int H1, int KO, co
   const size_t lds = vko > 0 ? (size_t)NT1 * 16 * 2 * 2 * sizeof(float4) : 0;
 #define MSC_MLP2_LAUNCH(TBV, WPE, VKO)                                                                              \
   hipLaunchKernelGGL((mlp2_relu_kernel<TBV, WPE, VKO>), grid, block, lds, st, x, n, L, KS1, NT1, w1, b1, w3, b3, KO, \
-                     out, pre1, grp, mlp_prio())
+                     out, pre1, grp, mlp_prio(), sm)
 #define MSC_MLP2_VKO(TBV, WPE)                  \
   switch (vko) {                                \
     case 1: MSC_MLP2_LAUNCH(TBV, WPE, 1); break; \

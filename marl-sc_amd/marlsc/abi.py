@@ -77,6 +77,12 @@ _VARIANT = os.environ.get("MSC_LIB_VARIANT", "")
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / (f"libmarlsc_{_VARIANT}.so" if _VARIANT else "libmarlsc.so")
 
 
+class MscGaussianEpilogue(C.Structure):
+    """msc_gaussian_epilogue (include/marlsc.h): the fused MLPs' action-sampling epilogue."""
+    _fields_ = [("log_std", C.c_void_p), ("log_std_rows", C.c_int32), ("logstd_floor", C.c_float),
+                ("eps", C.c_void_p), ("actions", C.c_void_p), ("logp", C.c_void_p), ("clipped", C.c_void_p)]
+
+
 def lib() -> C.CDLL:
     """Load libmarlsc.so (built by __graft_entry__.build()). Raises if it is missing."""
     global _LIB
@@ -121,6 +127,10 @@ def lib() -> C.CDLL:
                                         vp, vp, vp, C.c_int32, vp]
     L.msc_mlp2_relu_forward.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp,
                                         C.c_int32, vp]
+    L.msc_mlp3_relu_forward_sampled.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp,
+                                                vp, vp, vp, vp, vp, C.c_int32, P(MscGaussianEpilogue), vp]
+    L.msc_mlp2_relu_forward_sampled.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp, vp, vp,
+                                                vp, C.c_int32, P(MscGaussianEpilogue), vp]
     L.msc_meanstd_scratch_doubles.argtypes = [C.c_int64, C.c_int32]
     L.msc_meanstd_scratch_doubles.restype = C.c_int64
     L.msc_meanstd_filter.argtypes = [vp, vp, C.c_int64, C.c_int32, vp, C.c_int32, vp, vp, C.c_double, C.c_double, vp]
@@ -144,5 +154,6 @@ EXPORTED_SYMBOLS = [
     "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_timing", "msc_env_read_timing", "msc_env_read_timing_ea", "msc_env_obs_flat",
     "msc_env_read_state", "msc_env_state_bytes", "msc_env_save_state", "msc_env_load_state", "msc_env_check",
     "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_w3_layout", "msc_mlp3_relu_forward", "msc_mlp2_relu_forward",
+    "msc_mlp3_relu_forward_sampled", "msc_mlp2_relu_forward_sampled",
     "msc_meanstd_scratch_doubles", "msc_meanstd_filter", "msc_seedseq_u32", "msc_last_error", "msc_abi_version",
 ]

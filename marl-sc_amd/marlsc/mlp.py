@@ -141,12 +141,20 @@ class _Pack:
         self.key, self.tensors, self.stream, self.event = None, None, None, None
 
 
+def sample_fusable(mods) -> bool:
+    """True when the fused kernel for mods can also sample the actions (VALU output layer)."""
+    return fused_layers(mods) > 0 and w3_layout(mods[-1].out_features) == 1
+
+
 def mlp3_forward(mods, x: torch.Tensor, out: Optional[torch.Tensor] = None, *, w1: Optional[torch.Tensor] = None,
-                 pre1: Optional[torch.Tensor] = None, group: int = 1) -> torch.Tensor:
+                 pre1: Optional[torch.Tensor] = None, group: int = 1, sample=None) -> torch.Tensor:
     """The fused kernel over x [..., L] (f32 CUDA) -> [..., KO]; mods as accepted by fusable()
     (Linear-ReLU-Linear-ReLU-Linear or Linear-ReLU-Linear).
     w1: a first-layer weight to use instead of mods[0].weight (e.g. its local-feature columns);
-    pre1 [rows / group, H1]: added to the first layer's pre-activation of row n as pre1[n // group]."""
+    pre1 [rows / group, H1]: added to the first layer's pre-activation of row n as pre1[n // group].
+    sample: (log_std [P, KO], logstd_floor, eps, actions, logp, clipped) -- msc_gaussian_sample fused
+    into the kernel's epilogue (sample_fusable(mods) must hold); the means then go to `out` only when
+    it is given (returns `out`, possibly None)."""
     nl = fused_layers(mods)
     if nl == 0:
         raise ValueError("no fused kernel for this layer sequence (see fused_layers)")
@@ -188,11 +196,29 @@ def mlp3_forward(mods, x: torch.Tensor, out: Optional[torch.Tensor] = None, *, w
         pre1 = pre1.float().contiguous()
         if group < 1 or n % group or pre1.shape != (n // group, l1.out_features):
             raise ValueError(f"pre1 must be [{n // max(group, 1)}, {l1.out_features}] for {n} rows in groups of {group}")
-    if out is None:
-        out = torch.empty((n, KO), device=x.device, dtype=torch.float32)
     vp = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
     st = C.c_void_p(cur.cuda_stream)
     b1, b3 = (m.bias.detach().float().contiguous() for m in (l1, l3))
+    if sample is not None:
+        ls, floor, eps, act, logp, clipped = sample
+        for t in (ls, eps, act, logp, clipped):
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+                raise ValueError("sampling buffers must be contiguous float32 CUDA tensors")
+        if eps.numel() != n * KO or act.numel() != n * KO or clipped.numel() != n * KO or logp.numel() != n \
+                or ls.dim() != 2 or ls.shape[1] != KO:
+            raise ValueError("sampling buffers do not match the MLP's rows / outputs")
+        ep = abi.MscGaussianEpilogue(vp(ls), int(ls.shape[0]), C.c_float(floor), vp(eps), vp(act), vp(logp), vp(clipped))
+        if l2 is None:
+            abi.check(abi.lib().msc_mlp2_relu_forward_sampled(vp(xf), n, L, l1.out_features, KO, vp(w1p), vp(b1), vp(w3p),
+                                                              vp(b3), vp(out), vp(pre1), int(group), C.byref(ep), st))
+        else:
+            b2 = l2.bias.detach().float().contiguous()
+            abi.check(abi.lib().msc_mlp3_relu_forward_sampled(vp(xf), n, L, l1.out_features, l2.out_features, KO,
+                                                              vp(w1p), vp(b1), vp(w2p), vp(b2), vp(w3p), vp(b3), vp(out),
+                                                              vp(pre1), int(group), C.byref(ep), st))
+        return None if out is None else out.reshape(*lead, KO)
+    if out is None:
+        out = torch.empty((n, KO), device=x.device, dtype=torch.float32)
     if l2 is None:
         abi.check(abi.lib().msc_mlp2_relu_forward(vp(xf), n, L, l1.out_features, KO, vp(w1p), vp(b1), vp(w3p), vp(b3),
                                                   vp(out), vp(pre1), int(group), st))

@@ -49,7 +49,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from .rollout import MLP, RolloutCollector, RolloutConfig, split_global_mlp
+from .rollout import MLP, RolloutCollector, RolloutConfig, fused_actor_sample, mlp_forward, split_global_mlp
 
 LOG2PI = math.log(2 * math.pi)
 ENTROPY_CONST = 0.5 * math.log(2 * math.pi * math.e)
@@ -177,10 +177,23 @@ class MultiAgentActorCritic(nn.Module):
             return fn(self.policies[0], x)
         return torch.stack([fn(p, x[..., w, :]) for w, p in enumerate(self.policies)], dim=-2)
 
+    def actor_mean(self, local_obs, full_obs=None):
+        return self._per_agent(lambda p, v: p.actor(v), self._x(local_obs, full_obs, self.rc.actor_obs_type))
+
+    def log_std_table(self) -> torch.Tensor:
+        """[P, K] unclamped log_std rows (P = 1 shared, W per agent) for msc_gaussian_sample, which
+        applies logstd_floor itself."""
+        return torch.stack([p.log_std.detach().float() for p in self.policies]).contiguous()
+
+    def actor_sample(self, local_obs, full_obs, sample) -> bool:
+        """Shared policy: the actor with the rollout's action sampling fused into its kernel."""
+        if not self.shared:
+            return False
+        return fused_actor_sample(self.policies[0].actor, self._x(local_obs, full_obs, self.rc.actor_obs_type), sample)
+
     def dist_inputs(self, local_obs, full_obs=None):
-        x = self._x(local_obs, full_obs, self.rc.actor_obs_type)
         floor = self.rc.logstd_floor
-        mean = self._per_agent(lambda p, v: p.actor(v), x)
+        mean = self.actor_mean(local_obs, full_obs)
         if self.shared:
             log_std = torch.clamp(self.policies[0].log_std, min=floor).expand_as(mean)
         else:
@@ -188,15 +201,15 @@ class MultiAgentActorCritic(nn.Module):
             log_std = log_std.expand_as(mean)
         return mean, log_std
 
-    def values(self, local_obs, full_obs=None):
+    def values(self, local_obs, full_obs=None, out=None):
         if self.rc.critic_obs_type == "global" and full_obs is None:  # split first layer (rollout.py)
             if self.shared:
-                return split_global_mlp(self.policies[0].critic, local_obs).squeeze(-1)
+                return split_global_mlp(self.policies[0].critic, local_obs, out=out).squeeze(-1)
             return torch.stack([split_global_mlp(p.critic, local_obs, w).squeeze(-1)
                                 for w, p in enumerate(self.policies)], dim=-1)
         x = self._x(local_obs, full_obs, self.rc.critic_obs_type)
         if self.shared:
-            return self.policies[0].critic(x).squeeze(-1)
+            return mlp_forward(self.policies[0].critic, x, out=out).squeeze(-1)
         return torch.stack([p.critic(x[..., w, :]).squeeze(-1) for w, p in enumerate(self.policies)], dim=-1)
 
 

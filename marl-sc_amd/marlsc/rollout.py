@@ -62,15 +62,25 @@ class MLP(nn.Sequential):
 _FUSED = os.environ.get("MSC_FUSED_MLP", "1") != "0"
 
 
-def mlp_forward(layers, x: torch.Tensor, start: int = 0) -> torch.Tensor:
-    """layers[start:] applied to x (an nn.Sequential of Linear / activation modules)."""
+def _out_rows(out: Optional[torch.Tensor], rows: int, n_out: int) -> Optional[torch.Tensor]:
+    """`out` as the fused kernel's [rows, n_out] output buffer, or None when it cannot be one."""
+    if out is None or not out.is_contiguous() or out.dtype != torch.float32 or out.numel() != rows * n_out:
+        return None
+    return out.view(rows, n_out)
+
+
+def mlp_forward(layers, x: torch.Tensor, start: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """layers[start:] applied to x (an nn.Sequential of Linear / activation modules). `out`: a
+    buffer the fused kernel may write the result into (the caller checks the returned pointer)."""
     mods = list(layers)[start:]
     if not (_FUSED and x.is_cuda and not torch.is_grad_enabled()):
         for m in mods:
             x = m(x)
         return x
     if mlp3.ENABLED and x.dtype == torch.float32 and mlp3.fusable(mods):
-        return mlp3_forward(mods, x)  # the whole MLP as one f32-MFMA kernel (csrc/mlp.hip)
+        n_out = mods[-1].out_features
+        # the whole MLP as one f32-MFMA kernel (csrc/mlp.hip)
+        return mlp3_forward(mods, x, _out_rows(out, x.numel() // x.shape[-1], n_out))
     i = 0
     while i < len(mods):
         m = mods[i]
@@ -126,24 +136,38 @@ class ActorCritic(nn.Module):
 
     def dist_inputs(self, local_obs: torch.Tensor, full_obs: Optional[torch.Tensor] = None):
         """(mean, log_std) -- ACTION_DIST_INPUTS split in two."""
-        x = full_obs if self.rc.actor_obs_type == "global" else local_obs
-        mean = self.actor(x)
+        mean = self.actor_mean(local_obs, full_obs)
         log_std = torch.clamp(self.log_std, min=self.rc.logstd_floor).expand_as(mean)
         return mean, log_std
 
-    def values(self, local_obs: torch.Tensor, full_obs: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def actor_mean(self, local_obs: torch.Tensor, full_obs: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self.actor(full_obs if self.rc.actor_obs_type == "global" else local_obs)
+
+    def log_std_table(self) -> torch.Tensor:
+        """[1, K] unclamped log_std for msc_gaussian_sample (the kernel applies logstd_floor)."""
+        return self.log_std.detach().float().reshape(1, -1).contiguous()
+
+    def actor_sample(self, local_obs: torch.Tensor, full_obs: Optional[torch.Tensor], sample) -> bool:
+        """The actor forward with the action sampling fused into its kernel (see fused_actor_sample)."""
+        return fused_actor_sample(self.actor, full_obs if self.rc.actor_obs_type == "global" else local_obs, sample)
+
+    def values(self, local_obs: torch.Tensor, full_obs: Optional[torch.Tensor] = None,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """V [..., W]; `out` (contiguous, that shape) receives it when the fused critic runs."""
         if self.rc.critic_obs_type == "global" and full_obs is None:
-            return split_global_mlp(self.critic, local_obs).squeeze(-1)
+            return split_global_mlp(self.critic, local_obs, out=out).squeeze(-1)
         x = full_obs if self.rc.critic_obs_type == "global" else local_obs
-        return self.critic(x).squeeze(-1)
+        return mlp_forward(self.critic, x, out=out).squeeze(-1)
 
 
-def split_global_mlp(mlp: nn.Sequential, local_obs: torch.Tensor, agent: Optional[int] = None) -> torch.Tensor:
+def split_global_mlp(mlp: nn.Sequential, local_obs: torch.Tensor, agent: Optional[int] = None,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """An MLP over the per-agent flat input local_w || (local_0 .. local_{W-1}) evaluated from the
     local observations [..., W, L] without materialising it: the first Linear's columns split into
     a local block (per agent) and a global block (once per env, shared by its W agents) --
     mathematically the same layer, ~W x fewer first-layer flops and no [E, W, L(1+W)] buffer.
-    agent=None: all W agents ([..., W, out]); agent=w: agent w only ([..., out])."""
+    agent=None: all W agents ([..., W, out]); agent=w: agent w only ([..., out]).
+    out: a contiguous buffer of the fused kernel's output (rows x outputs), used when it runs."""
     first = mlp[0]
     W, L = local_obs.shape[-2], local_obs.shape[-1]
     glob = local_obs.reshape(*local_obs.shape[:-2], W * L)
@@ -153,13 +177,26 @@ def split_global_mlp(mlp: nn.Sequential, local_obs: torch.Tensor, agent: Optiona
         # the whole critic as one f32-MFMA kernel over the E*W rows, with the per-env global block
         # (one GEMM over E rows) added to the first layer of each of the env's W rows
         g = torch.nn.functional.linear(glob.reshape(-1, W * L), first.weight[:, L:])  # b1: in the kernel
-        return mlp3_forward(mods, local_obs, w1=first.weight[:, :L], pre1=g, group=W)
+        o = _out_rows(out, local_obs[..., 0].numel(), mods[-1].out_features)
+        return mlp3_forward(mods, local_obs, o, w1=first.weight[:, :L], pre1=g, group=W)
     g = torch.nn.functional.linear(glob, first.weight[:, L:])
     if agent is None:
         h = torch.nn.functional.linear(local_obs, first.weight[:, :L], first.bias) + g.unsqueeze(-2)
     else:
         h = torch.nn.functional.linear(local_obs[..., agent, :], first.weight[:, :L], first.bias) + g
     return mlp_forward(mlp, h, 1)
+
+
+def fused_actor_sample(actor: nn.Sequential, x: torch.Tensor, sample) -> bool:
+    """Run `actor` over x with msc_gaussian_sample fused into the MLP kernel's epilogue (sample =
+    (log_std [P, K], logstd_floor, eps, actions, logp, clipped)); False (nothing launched) when the
+    fused kernel does not apply, e.g. more than 8 outputs or a non-ReLU MLP."""
+    mods = list(actor)
+    if not (_FUSED and mlp3.ENABLED and x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
+            and mlp3.sample_fusable(mods)):
+        return False
+    mlp3_forward(mods, x, None, sample=sample)
+    return True
 
 
 def _vp(t: Optional[torch.Tensor]):
@@ -288,6 +325,9 @@ class RolloutCollector:
         cs = os.environ.get("MSC_ROLLOUT_CRITIC_SIDE")
         self._critic_side = (self.N <= 65536 if cs is None else cs != "0") and not self._need_flat
         self._gen = torch.Generator(device=dev).manual_seed(seed)
+        import inspect
+        self._values_out = "out" in inspect.signature(module.values).parameters
+        self._ls: Optional[torch.Tensor] = None
         # obs_normalization "meanstd": RLlib's running filter, one per lane (env runner), synchronised
         # after every collect (marlsc/obs_filter.py)
         self.obs_filter = None
@@ -306,30 +346,53 @@ class RolloutCollector:
     def _full(self, ln: _Lane, obs):
         return ln.env.obs_flat(obs=obs, out=ln.flat) if self._need_flat else None
 
+    def _values_into(self, t: int, sl: slice, obs, full) -> None:
+        """V(obs_t) into values[t, sl]: written by the fused critic kernel directly when the module
+        takes an output buffer, copied otherwise."""
+        dst = self.values[t, sl]
+        v = self.module.values(obs, full, out=dst) if self._values_out else self.module.values(obs, full)
+        if v.data_ptr() != dst.data_ptr():
+            dst.copy_(v)
+
+    def _critic_on_side(self, ln: _Lane, t: int, sl: slice, obs, full) -> None:
+        if ln.critic_stream is None:
+            ln.critic_stream = torch.cuda.Stream(device=obs.device)
+        ev = torch.cuda.Event()
+        ev.record()
+        ln.critic_stream.wait_event(ev)
+        with torch.cuda.stream(ln.critic_stream):
+            self._values_into(t, sl, obs, full)
+
     def _step(self, ln: _Lane, t: int) -> None:
         env, m, sl = ln.env, self.module, slice(ln.e0, ln.e1)
         obs = self._obs_all[t, sl]
         full = self._full(ln, obs)
         if self._critic_side:
-            if ln.critic_stream is None:
-                ln.critic_stream = torch.cuda.Stream(device=obs.device)
-            ev = torch.cuda.Event()
-            ev.record()
-            ln.critic_stream.wait_event(ev)
-            with torch.cuda.stream(ln.critic_stream):
-                self.values[t, sl] = m.values(obs, full)
-        mean, log_std = m.dist_inputs(obs, full)
-        if not self._critic_side:
-            self.values[t, sl] = m.values(obs, full)
+            self._critic_on_side(ln, t, sl, obs, full)
         # standard-normal noise for NOISE_CHUNK steps of the lane at once (one launch instead of one
         # per step)
         if t % NOISE_CHUNK == 0:
             n = min(NOISE_CHUNK, self.T - t)
-            ln.noise = torch.randn((n,) + tuple(mean.shape), device=mean.device, generator=self._gen)
+            ln.noise = torch.randn((n,) + tuple(self.actions[t, sl].shape), device=obs.device, generator=self._gen)
         eps = ln.noise[t % NOISE_CHUNK]
-        # sample, log-density and the env's clip in one HIP kernel (msc_gaussian_sample)
-        # log_std [E, W, K] is a broadcast of one row (shared policy) or of W rows (per agent)
-        a = gaussian_sample(mean.contiguous(), log_std[0], m.rc.logstd_floor, eps, self.actions[t, sl], self.logp[t, sl])
+        a = None
+        if self._ls is not None and hasattr(m, "actor_sample"):
+            # actor forward + sampling + log-density + the env's clip in one kernel launch
+            clipped = torch.empty_like(self.actions[t, sl])
+            if m.actor_sample(obs, full, (self._ls, m.rc.logstd_floor, eps, self.actions[t, sl], self.logp[t, sl],
+                                          clipped)):
+                a = clipped
+        if a is None:
+            if self._ls is not None:  # the module's raw log_std rows, taken once per collect
+                mean, ls = m.actor_mean(obs, full), self._ls
+            else:
+                mean, log_std = m.dist_inputs(obs, full)
+                ls = log_std[0]
+            # sample, log-density and the env's clip in one HIP kernel (msc_gaussian_sample)
+            # (log_std rows: one shared row or one per agent, repeating every P rows)
+            a = gaussian_sample(mean.contiguous(), ls, m.rc.logstd_floor, eps, self.actions[t, sl], self.logp[t, sl])
+        if not self._critic_side:
+            self._values_into(t, sl, obs, full)
         may_end = env.may_truncate()
         _, _, trunc, final_obs = env.step(a, obs_out=self._obs_all[t + 1, sl], rewards_out=self.rewards[t, sl],
                                           truncated_out=self._trunc_env[t, sl])
@@ -351,6 +414,9 @@ class RolloutCollector:
         m, T = self.module, self.T
         main = torch.cuda.current_stream()
         self.next_values.zero_()
+        # log_std does not change during a collect: its rows go to the sampling kernel as they are
+        # (the kernel clamps at logstd_floor), no clamp / broadcast launches per step
+        self._ls = m.log_std_table() if hasattr(m, "log_std_table") and hasattr(m, "actor_mean") else None
         for ln in self._lanes:
             if os.environ.get("MSC_ROLLOUT_CHAIN_PRIO", "0") != "0" and not getattr(ln, "prio_set", False):
                 # A/B: step chain ahead of the next step's demand kernel (neutral: 1.234 vs 1.228 ms

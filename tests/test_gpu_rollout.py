@@ -221,6 +221,52 @@ def test_fused_mlp_forms_match_torch_layers(L, hidden, KO, n):
         torch.testing.assert_close(mlp3_forward(mods, x), ref(), rtol=2e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("L,hidden,KO,P,n", [
+    (34, [256, 256], 5, 1, 32768),  # MAPPO actor, shared log_std row
+    (34, [256], 5, 8, 4096 * 8),    # IPPO actor [256], one log_std row per agent
+    (13, [64, 64], 2, 2, 1001),
+    (34, [96], 8, 4, 77),
+])
+def test_fused_actor_sampling_equals_mlp_then_gaussian_kernel(L, hidden, KO, P, n):
+    # msc_mlp{2,3}_relu_forward_sampled: the sampling epilogue is msc_gaussian_sample's arithmetic on
+    # the kernel's own outputs, so actions / logp / clipped equal the two-launch path bit for bit
+    from marlsc.mlp import mlp3_forward, sample_fusable
+    from marlsc.rollout import MLP, gaussian_sample
+    torch.manual_seed(L + KO + P)
+    mods = list(MLP(L, KO, {"hidden_sizes": hidden}).cuda())
+    assert sample_fusable(mods)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(n, L, device="cuda", generator=g)
+    eps = torch.randn(n, KO, device="cuda", generator=g)
+    ls = (torch.randn(P, KO, device="cuda", generator=g) - 1.0).contiguous()
+    with torch.no_grad():
+        mean = mlp3_forward(mods, x)
+        a_ref, lp_ref = torch.empty_like(mean), torch.empty(n, device="cuda")
+        c_ref = gaussian_sample(mean, ls, -2.0, eps, a_ref, lp_ref)
+        a, lp, c, m_out = torch.empty_like(mean), torch.empty(n, device="cuda"), torch.empty_like(mean), torch.empty_like(mean)
+        mlp3_forward(mods, x, m_out, sample=(ls, -2.0, eps, a, lp, c))
+        a2, lp2, c2 = torch.empty_like(mean), torch.empty(n, device="cuda"), torch.empty_like(mean)
+        assert mlp3_forward(mods, x, None, sample=(ls, -2.0, eps, a2, lp2, c2)) is None  # means not written
+    assert torch.equal(m_out, mean)
+    for got in ((a, lp, c), (a2, lp2, c2)):
+        assert torch.equal(got[0], a_ref) and torch.equal(got[1], lp_ref) and torch.equal(got[2], c_ref)
+
+
+def test_rollout_with_fused_sampling_equals_the_two_launch_path(monkeypatch):
+    # the collector's fused actor + sampling launch against its mean -> msc_gaussian_sample path on
+    # the same env seeds and noise: every buffer identical
+    out = []
+    for fused in (True, False):
+        spec, env, m, col = _setup("global", E=128, T=9, ep_len=5)
+        if not fused:
+            monkeypatch.setattr(type(m), "actor_sample", lambda self, *a, **k: False)
+        b = col.collect()
+        out.append({k: v.clone() for k, v in b.items()})
+        monkeypatch.undo()
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
+
+
 def test_fused_mlp_rejects_unsupported_shapes():
     from marlsc.mlp import fused_layers
     from marlsc.rollout import MLP

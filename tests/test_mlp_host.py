@@ -127,6 +127,29 @@ def test_mlp3_abi_rejects_bad_arguments_before_any_launch():
     assert b"in_dim" in L.msc_last_error()
 
 
+def test_sampled_mlp_entry_points_validate_arguments():
+    # msc_mlp{3,2}_relu_forward_sampled reject a missing epilogue, missing sampling buffers and
+    # output layers the epilogue does not cover (> 8 outputs) before any launch
+    import ctypes as C
+    from marlsc import abi
+    L = abi.lib()
+    p = C.c_void_p(256)
+    ep = abi.MscGaussianEpilogue(p, 1, C.c_float(-3.5), p, p, p, p)
+    f = L.msc_mlp3_relu_forward_sampled
+    assert f(p, 8, 34, 256, 256, 5, p, p, p, p, p, p, None, None, 1, None, None) == -1
+    assert b"null" in L.msc_last_error()
+    assert f(p, 8, 34, 256, 256, 9, p, p, p, p, p, p, None, None, 1, C.byref(ep), None) == -1
+    assert b"VALU output layer" in L.msc_last_error()
+    bad = abi.MscGaussianEpilogue(p, 0, C.c_float(-3.5), p, p, p, p)
+    assert f(p, 8, 34, 256, 256, 5, p, p, p, p, p, p, None, None, 1, C.byref(bad), None) == -1
+    assert b"log_std_rows" in L.msc_last_error()
+    g = L.msc_mlp2_relu_forward_sampled
+    nul = abi.MscGaussianEpilogue(p, 1, C.c_float(-3.5), None, p, p, p)
+    assert g(p, 8, 34, 256, 5, p, p, p, p, None, None, 1, C.byref(nul), None) == -1
+    assert b"null sampling buffer" in L.msc_last_error()
+    assert L.msc_mlp3_relu_forward(p, 8, 34, 256, 256, 5, p, p, p, p, p, p, None, None, 1, None) == -1  # out required
+
+
 def test_output_layer_layout_rule():
     from marlsc.mlp import w3_layout
     assert [w3_layout(k) for k in (1, 5, 8)] == [1, 1, 1]  # VALU output layer up to 8 outputs
