@@ -224,8 +224,8 @@ def test_fused_mlp_forms_match_torch_layers(L, hidden, KO, n):
 @pytest.mark.parametrize("L,hidden,KO,P,n", [
     (34, [256, 256], 5, 1, 32768),  # MAPPO actor, shared log_std row
     (34, [256], 5, 8, 4096 * 8),    # IPPO actor [256], one log_std row per agent
-    (13, [64, 64], 2, 2, 1001),
-    (34, [96], 8, 4, 77),
+    (13, [64, 64], 2, 2, 1002),   # ragged last tile
+    (34, [96], 8, 4, 76),
 ])
 def test_fused_actor_sampling_equals_mlp_then_gaussian_kernel(L, hidden, KO, P, n):
     # msc_mlp{2,3}_relu_forward_sampled: the sampling epilogue is msc_gaussian_sample's arithmetic on
