@@ -34,7 +34,7 @@ struct EnvConst {
   int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
   int32_t parser_rot;   // which wave of a demand block parses: (wave + rot(block)) % (1 + G) == 0 (A/B knob)
   int32_t obs_stage;    // 1: step_c stages each wave's observations in LDS and writes them coalesced
-  int32_t obs_ring_reg; // 1: step_c (<= 8 warehouses) reads the pending ring into registers before its stores
+  int32_t obs_ring_reg; // 1: step_a / step_c (<= 8 warehouses) read the pending ring into registers before their stores
   int32_t epw_dem;      // envs per 64-lane block of the demand kernel (64, 32 or 16; see launch_demand)
   int32_t shared_home;  // 1: some region is the home region of two or more warehouses
   int32_t demand_uni;   // 1: Poisson parameters equal across regions (demand_unit_kernel<UNI>)

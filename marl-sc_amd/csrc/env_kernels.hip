@@ -1068,7 +1068,13 @@ __global__ void ea_materialize_kernel(const DevEnv* __restrict__ dp, int32_t slo
 // scratch (EnvState::sc_*), and [i][E] state stays coalesced for the wave = warehouse phases.
 // ------------------------------------------------------------------------------------------
 // ---- phase A ------------------------------------------------------------------------------
-template <int K, bool DBG>
+#ifndef MSC_SA_RING_REG
+#define MSC_SA_RING_REG 4  // step_a: pending rings of up to this many slots are read into registers
+#endif
+constexpr int SA_RING_REG = MSC_SA_RING_REG;
+// REG: the register-ring instantiation (the fixed-lead path holds the K rings in registers: ~2x the
+// VGPRs, which costs co-residency beside the demand kernel at 32,768 envs; used with obs_ring_reg)
+template <int K, bool DBG, bool REG = false>
 __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
@@ -1108,6 +1114,70 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __
   const int w = wave, t = Lt[lane];
   const int slot = t % RING;
   double inbF = 0.0, inbV = 0.0;
+  if constexpr (REG && K <= 5) {
+  if (RING <= SA_RING_REG && !stoch) {
+    // (fixed lead times; <= 5 SKUs, whose rings fit the register budget) Every load of the K SKUs first, then the arithmetic, then the stores: vector loads and stores
+    // retire through one counter (vmcnt), so a load issued after a store waits for it (the loop
+    // below stores the new order before it reads the ring for arrivals, K times)
+    float a[K];
+    int inc_old[K], inv[K], rv[K][SA_RING_REG];
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      a[sk] = io.actions[(e * W + w) * K + sk];
+      inc_old[sk] = s.inc[i * E + e];
+      inv[sk] = s.inv[i * E + e];
+      const int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
+#pragma unroll
+      for (int q = 0; q < SA_RING_REG; q++) rv[sk][q] = q < RING ? rq[q * E] : 0;
+    }
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      int pend = 0;
+#pragma unroll
+      for (int q = 0; q < SA_RING_REG; q++) pend += rv[sk][q];
+      const double prm = c.act_param[sk];  // _rescale_actions_to_quantities (multi_env.py:795-848)
+      double q;
+      if (c.action_type == MSC_ACTION_DIRECT) {
+        q = rint((double)((a[sk] + 1.0f) / 2.0f) * prm);
+        q = q < 0.0 ? 0.0 : (q > prm ? prm : q);
+      } else if (c.action_type == MSC_ACTION_DEMAND_CENTERED) {
+        q = rint(prm * (double)a[sk]) + (double)inc_old[sk];
+        q = q < 0.0 ? 0.0 : q;
+      } else {
+        const double target = (double)((a[sk] + 1.0f) / 2.0f) * prm;
+        q = rint((target - (double)(float)inc_old[sk]) - (double)(float)pend);
+        q = q < 0.0 ? 0.0 : q;
+      }
+      const int qi = (int)q;
+      const int elt = c.elt[i];
+      int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
+      if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = inv[sk];
+      // _apply_arrivals: orders whose actual lead time equals their age arrive (actual arrival == t)
+      int iv = inv[sk];
+#pragma unroll
+      for (int jr = 0; jr < SA_RING_REG; jr++) {
+        int age = (t - jr) % RING;
+        if (age < 0) age += RING;
+        const bool arrive = jr < RING && jr != slot && rv[sk][jr] != 0 && elt == age;
+        iv += arrive ? rv[sk][jr] : 0;
+        if (arrive) rq[jr * E] = 0;
+      }
+      rq[slot * E] = qi;  // _apply_orders: the slot of order time t
+      s.inv[i * E + e] = iv;
+      s.inc[i * E + e] = 0;
+      if (qi > 0) inbF += c.inF[i];
+      inbV += ((double)qi * c.skw[sk]) * c.inV[i];
+      if (dbg) {
+        if (info.pending_total) info.pending_total[e * WK + i] = pend;
+        if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
+      }
+    }
+    s.sc_inb[w * E + e] = inbF + inbV;
+    return;
+  }
+  }
 #pragma unroll
   for (int sk = 0; sk < K; sk++) {
     const int i = w * K + sk;
@@ -1826,7 +1896,8 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
   // three phase kernels, group-per-env allocation
   const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : c.W <= 8 ? 8 : 16;
   const bool dbg = io.has_info != 0;  // collect_step_info: the instrumented instantiations
-  KFn a = dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>;
+  KFn a = c.obs_ring_reg ? (dbg ? (KFn)step_a_kernel<K, true, true> : (KFn)step_a_kernel<K, false, true>)
+                         : (dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>);
   KFn cc = (c.W <= 8 && c.obs_ring_reg) ? (dbg ? (KFn)step_c_kernel<K, true, 8> : (KFn)step_c_kernel<K, false, 8>)
                     : (dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>);
   const bool tab = step_b_tab_bytes(c.R, c.W) <= STEP_B_TAB_MAX;

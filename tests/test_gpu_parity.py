@@ -31,6 +31,10 @@ def _set_alloc(monkeypatch, param):
         monkeypatch.setenv("MSC_ALLOC_SORT", "1" if sort[0] == "sorted" else "0")
     else:
         monkeypatch.delenv("MSC_ALLOC_SORT", raising=False)
+    # step_a / step_c with the pending ring in registers: off with the lane kernel (as the library
+    # runs at >= 16,384 envs, C3), on with the others (its default below that), so both forms of the
+    # two phase kernels meet every reference
+    monkeypatch.setenv("MSC_OBS_RING_REG", "0" if impl.startswith("lane") else "1")
     ea = "0" if "ea0" in opts or impl.startswith("lane") else "1" if ("ea1" in opts or impl == "scan") else None
     if ea is None:
         monkeypatch.delenv("MSC_EA", raising=False)
