@@ -1178,6 +1178,58 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __
     return;
   }
   }
+  if (RING <= SA_RING_REG && !stoch) {
+    // (the low-register form: one SKU at a time, each SKU's loads issued together before its stores)
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
+      const float a = io.actions[(e * W + w) * K + sk];
+      const int inc_old = s.inc[i * E + e];
+      int iv = s.inv[i * E + e];
+      int rv[SA_RING_REG];
+#pragma unroll
+      for (int q = 0; q < SA_RING_REG; q++) rv[q] = q < RING ? rq[q * E] : 0;
+      int pend = 0;
+#pragma unroll
+      for (int q = 0; q < SA_RING_REG; q++) pend += rv[q];
+      const double prm = c.act_param[sk];  // _rescale_actions_to_quantities (multi_env.py:795-848)
+      double q;
+      if (c.action_type == MSC_ACTION_DIRECT) {
+        q = rint((double)((a + 1.0f) / 2.0f) * prm);
+        q = q < 0.0 ? 0.0 : (q > prm ? prm : q);
+      } else if (c.action_type == MSC_ACTION_DEMAND_CENTERED) {
+        q = rint(prm * (double)a) + (double)inc_old;
+        q = q < 0.0 ? 0.0 : q;
+      } else {
+        const double target = (double)((a + 1.0f) / 2.0f) * prm;
+        q = rint((target - (double)(float)inc_old) - (double)(float)pend);
+        q = q < 0.0 ? 0.0 : q;
+      }
+      const int qi = (int)q;
+      const int elt = c.elt[i];
+      if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = iv;
+#pragma unroll
+      for (int jr = 0; jr < SA_RING_REG; jr++) {  // _apply_arrivals (actual arrival == t)
+        int age = (t - jr) % RING;
+        if (age < 0) age += RING;
+        const bool arrive = jr < RING && jr != slot && rv[jr] != 0 && elt == age;
+        iv += arrive ? rv[jr] : 0;
+        if (arrive) rq[jr * E] = 0;
+      }
+      rq[slot * E] = qi;  // _apply_orders: the slot of order time t
+      s.inv[i * E + e] = iv;
+      s.inc[i * E + e] = 0;
+      if (qi > 0) inbF += c.inF[i];
+      inbV += ((double)qi * c.skw[sk]) * c.inV[i];
+      if (dbg) {
+        if (info.pending_total) info.pending_total[e * WK + i] = pend;
+        if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
+      }
+    }
+    s.sc_inb[w * E + e] = inbF + inbV;
+    return;
+  }
 #pragma unroll
   for (int sk = 0; sk < K; sk++) {
     const int i = w * K + sk;
@@ -1712,16 +1764,24 @@ __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restric
     t = s.t[e];
     const int hslot = t % MSC_HISTORY;
     double hold = 0.0;
+    // the loads first, then the stores (a load issued after a store waits for it: one vmcnt)
+    int iv[K], v[K];
+    float fo[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       const int i = w * K + sk;
-      const int iv = s.inv[i * E + e];
-      const int v = s.inc[i * E + e];
-      s.hist[((int64_t)hslot * WK + i) * E + e] = v;
-      s.fc[i * E + e] = 0.3f * (float)v + 0.7f * s.fc[i * E + e];  // EMA forecast (f32)
-      hold += c.hold_per_sku ? (double)iv * c.hold[sk] : ((double)iv * c.skw[sk]) * c.hold_scalar;
+      iv[sk] = s.inv[i * E + e];
+      v[sk] = s.inc[i * E + e];
+      fo[sk] = s.fc[i * E + e];
     }
     const double pen = s.sc_pen[w * E + e], out = s.sc_out[w * E + e], inb = s.sc_inb[w * E + e];
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      s.hist[((int64_t)hslot * WK + i) * E + e] = v[sk];
+      s.fc[i * E + e] = 0.3f * (float)v[sk] + 0.7f * fo[sk];  // EMA forecast (f32)
+      hold += c.hold_per_sku ? (double)iv[sk] * c.hold[sk] : ((double)iv[sk] * c.skw[sk]) * c.hold_scalar;
+    }
     rw = -((((hold + pen) + out) + inb) * c.scale);
     Lrw[w * BS + lane] = rw;
     if (dbg && info.costs) {
