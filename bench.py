@@ -161,16 +161,19 @@ def c2_line(args, rank: int):
     # Episode-ahead demand refills 4 slots per launch, i.e. one generation launch per 4 episodes:
     # a timed window of 1,000 steps held 2 or 3 of them depending on its phase (0.214 / 0.246 ms per
     # step in consecutive windows, tools/ab_state.py), so the window is a whole number of refill
-    # periods (12 episodes = 3 periods), after a warm-up of the same length (episode 0 of the
-    # snapshot draws its demand per step while the first 11 episodes are generated)
+    # periods (24 episodes = 6 periods), after a warm-up of the same length: the snapshot's first 15
+    # episodes are generated in two bulk launches that keep the generation stream busy for the first
+    # ~20 episodes (a 12-episode window after 12 read 162 M where 48 episodes read 175.5 M,
+    # profiles/r03/ab_ea_slots.txt)
     period = 4 * T
-    steps = max(3 * period, -(-args.steps // period) * period)
-    warm = 3 * period
+    steps = max(6 * period, -(-args.steps // period) * period)
+    warm = 6 * period
     dt, tm = time_env(env, pool, steps, warm, 1)
     rc = RolloutConfig.from_algorithm_config(algo)
     torch.manual_seed(0)
     module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
-    t_roll = time_rollout(env, module, T, 1, seed=rank, warm=2, reps=2) if args.rollout_T > 0 else 0.0
+    # one refill period (4 episodes = 4 rollouts) timed, so the window holds one generation launch
+    t_roll = time_rollout(env, module, T, 1, seed=rank, warm=4, reps=4) if args.rollout_T > 0 else 0.0
     a_h, c_h = rc.actor["hidden_sizes"], rc.critic["hidden_sizes"]
     out = {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x {spec.K} SKUs "
                        f"(BASELINE configs[1])",

@@ -441,7 +441,9 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     if (d->demand_type == MSC_DEMAND_POISSON) {
       bool want = n_envs <= 8192;
       if (const char* ea = getenv("MSC_EA")) want = atoi(ea) != 0;
-      int S = 12;
+      // 16 slots: the generation runs further ahead of the step (C2 over 48 episodes: 175.5 M
+      // agent-steps/s at 12 slots, 180-183 M at 16; profiles/r03/ab_ea_slots.txt); 29 GB at 4,096 envs
+      int S = 16;
       if (const char* es = getenv("MSC_EA_SLOTS")) S = atoi(es);
       S = S < 2 ? 2 : (S > MSC_EA_MAX_S ? MSC_EA_MAX_S : S);
       if (want) {
@@ -610,7 +612,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       s.ea_cnt = s2.ea_cnt = (int32_t*)(b + al(rec) + al(offb) + al(posb));
       env->ea_enabled = true;
       // refill batch: a batch freed by episodes n-B+1 .. n is needed S-B episodes later
-      int B = S / 3 > 1 ? S / 3 : 1;
+      int B = S / 4 > 1 ? S / 4 : 1;
       if (const char* eb = getenv("MSC_EA_BATCH")) B = atoi(eb);
       env->ea_batch = B < 1 ? 1 : (B > S - 1 ? S - 1 : B);
       // step_c's observation staging (up to 80 KB of LDS per block) stalls behind a generation

@@ -471,7 +471,7 @@ def test_empirical_trace_demand_vs_oracle(W, R, lost):
     _lockstep(spec, 96, 14, seed=4, check_every=3)
 
 
-@pytest.mark.parametrize("slots,batch,chunk", [(4, 1, 10), (4, 2, 2), (6, 2, 4)])
+@pytest.mark.parametrize("slots,batch,chunk", [(4, 1, 10), (4, 2, 2), (6, 2, 4), (16, 4, 3)])
 def test_episode_ahead_equals_sequential(monkeypatch, slots, batch, chunk):
     # episode-ahead demand (whole future episodes drawn on a side stream)
     # against per-step sequential demand: identical observations, rewards and reported state
