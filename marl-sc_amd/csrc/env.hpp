@@ -23,7 +23,7 @@ namespace msc {
 
 constexpr int BS = 64;          // threads per block of the env kernels (one wave: one env per lane)
 constexpr int MAX_RING = 64;    // pending-order ring slots (max actual lead time + 1)
-#define MSC_EA_MAX_S 16   // episode-ahead demand: max episode slots per env
+#define MSC_EA_MAX_S 32   // episode-ahead demand: max episode slots per env
 
 struct EnvConst {
   int32_t W, K, R, T, Lmax, RING, F, L, order_cap;
