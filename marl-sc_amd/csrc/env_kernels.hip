@@ -168,7 +168,7 @@ __device__ __noinline__ void reset_env(const EnvConst& c, const EnvState& s, int
 constexpr int OBS_RING_REG = MSC_OBS_RING_REG;
 // RREG > 0: rings of up to RREG slots are read into registers (step_c with <= 8 waves per block;
 // elsewhere the register budget is 128 and the ring is read where it is used)
-template <int K, int RREG = 0>
+template <int K, int RREG = 0, bool HIST_STATIC = false>
 __device__ __forceinline__ void build_obs_agent(const EnvConst& c, const EnvState& s, int64_t e, int w, int t_now,
                                              int n_hist, const int32_t* shh, const int32_t* sht, int64_t sstride,
                                              float* out) {
@@ -203,7 +203,20 @@ __device__ __forceinline__ void build_obs_agent(const EnvConst& c, const EnvStat
       sa[sk] = sht ? sht[i * sstride] - sh[sk] : 0;
       fc[sk] = s.fc[i * E + e];
       int hs = 0;
-      for (int h = 0; h < n_hist; h++) hs += s.hist[(((t_now - n_hist + 1 + h) % MSC_HISTORY) * W * K + i) * E + e];
+      if constexpr (HIST_STATIC) {
+        // the MSC_HISTORY slot loads issued together (a counted loop waits on each): slot q holds the
+        // demand of age (t_now - q) mod MSC_HISTORY, in the window iff that age < n_hist (an integer
+        // sum: the order of the terms does not matter)
+        const int tm5 = t_now % MSC_HISTORY;
+#pragma unroll
+        for (int q = 0; q < MSC_HISTORY; q++) {
+          const int age = tm5 - q >= 0 ? tm5 - q : tm5 - q + MSC_HISTORY;
+          const int v = s.hist[((int64_t)q * W * K + i) * E + e];
+          hs += age < n_hist ? v : 0;
+        }
+      } else {
+        for (int h = 0; h < n_hist; h++) hs += s.hist[(((t_now - n_hist + 1 + h) % MSC_HISTORY) * W * K + i) * E + e];
+      }
       rm[sk] = n_hist > 0 ? (float)hs / (float)n_hist : 0.0f;
       pend_sum[sk] = 0;
     }
@@ -1745,6 +1758,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
 template <int K, bool DBG, int WB = MSC_MAX_W>
 __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   constexpr int RREG = WB <= 8 ? OBS_RING_REG : 0;
+  constexpr bool HSTAT = true;
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   extern __shared__ __attribute__((aligned(16))) double Lrw[];  // [W][BS] rewards (team sum)
@@ -1815,9 +1829,9 @@ __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restric
     const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
     trunc = t + 1 >= c.T;
     if (!trunc) {
-      build_obs_agent<K, RREG>(c, s, e, w, t, n_hist, shh, sht, E, c.obs_stage ? stg + lane * RS : io.obs + obs_off);
+      build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, c.obs_stage ? stg + lane * RS : io.obs + obs_off);
     } else if (io.final_obs) {
-      build_obs_agent<K, RREG>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
+      build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
     }
   }
   if (c.obs_stage) {
