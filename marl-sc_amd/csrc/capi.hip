@@ -397,8 +397,12 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     const char* prot = getenv("MSC_PARSER_ROT");
     c.parser_rot = prot ? atoi(prot) : 0;
     // step_c observation staging when the block's stage fits (C3: 8 x 64 x 35 floats = 70 KiB)
-    c.obs_stage = (size_t)BS * ((c.W * c.L) | 1) * sizeof(float) <= 80 * 1024 ? 1 : 0;
-    if (const char* os = getenv("MSC_OBS_STAGE")) c.obs_stage = c.obs_stage && atoi(os) != 0;
+    // staged in two phases of ceil(W / 2) agents: half the LDS, so two step_c blocks fit beside the
+    // pipelined demand kernel's (C3 MAPPO rollout 1.19 -> 1.14 ms per step; profiles/r03/ab_stage_phases.txt)
+    c.obs_stage = (size_t)BS * ((c.W * c.L) | 1) * sizeof(float) <= 80 * 1024 ? (c.W >= 2 ? 2 : 1) : 0;
+    // MSC_OBS_STAGE=0 | 1 | P: off / whole block / in P phases of ceil(W / P) agents (a P-th of the LDS)
+    if (const char* os = getenv("MSC_OBS_STAGE")) c.obs_stage = c.obs_stage ? (atoi(os) > 0 ? atoi(os) : 0) : 0;
+    if (c.obs_stage > c.W) c.obs_stage = c.W;
     // step_c with the pending ring in registers (8-wave blocks, up to 256 VGPRs): C2 (4,096 envs)
     // 152.7 -> 157.4 M agent-steps/s; at 32,768 envs the env line is unchanged and the MAPPO rollout
     // 1.165 -> 1.188 ms per step (fewer step_c blocks fit beside the demand kernel), so only below

@@ -1812,12 +1812,16 @@ __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restric
   // odd: a wave's 64 lanes write 64 different banks), then written to HBM as the block's one
   // contiguous [64][W][L] range, every cache line whole (per-agent vectors of L floats at a
   // stride of W*L floats leave partly written lines per store)
-  const int L = c.L, WL = W * L, RS = WL | 1;
+  // obs_stage = P > 1: the agents staged in P phases of ceil(W / P) (a P-th of the LDS, so P times
+  // as many blocks fit beside the demand kernel's; each phase's waves build, the block copies out)
+  const int L = c.L, WL = W * L;
+  const int P = c.obs_stage > 1 ? c.obs_stage : 1, WP = (W + P - 1) / P, RS = (WP * L) | 1;
   float* stg = reinterpret_cast<float*>(Lrw + W * BS);
   int32_t* Lskip = reinterpret_cast<int32_t*>(stg + BS * RS);  // [BS]: env's vector not staged
   // shipped home / total of this step, [(w*K+s) * E] from the env's column
   const int32_t* shh = s.sc_shh + e;
   const int32_t* sht = s.sc_sht + e;
+  const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
   if (act) {
     double v = rw;
     if (c.scope == MSC_SCOPE_TEAM) {  // team scope: sum over agents in agent order
@@ -1826,31 +1830,35 @@ __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restric
     }
     io.rew[e * W + w] = (float)v;
     if (io.rew64) io.rew64[e * W + w] = v;
-    const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
     trunc = t + 1 >= c.T;
-    if (!trunc) {
-      build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, c.obs_stage ? stg + lane * RS : io.obs + obs_off);
-    } else if (io.final_obs) {
-      build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
-    }
+    if (trunc && io.final_obs) build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
+    if (!trunc && !c.obs_stage) build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, io.obs + obs_off);
   }
   if (c.obs_stage) {
     if (wave == 0) Lskip[lane] = (e >= E || trunc) ? 1 : 0;
-    __syncthreads();
     const int64_t e0 = (int64_t)blockIdx.x * BS;
     const int nenv = E - e0 < BS ? (int)(E - e0) : BS;
-    const int n = nenv * WL, nt = (int)blockDim.x;
-    const int dq = nt / WL, dr = nt % WL;  // (env, column) step of the flat index per iteration
-    int ev = (int)threadIdx.x / WL, j = (int)threadIdx.x % WL;
-    float* dst = io.obs + e0 * WL;
-    for (int i = (int)threadIdx.x; i < n; i += nt) {
-      if (!Lskip[ev]) dst[i] = stg[ev * RS + j];
-      j += dr;
-      ev += dq;
-      if (j >= WL) {
-        j -= WL;
-        ev += 1;
+    const int nt = (int)blockDim.x;
+    for (int p = 0; p < P; p++) {
+      const int w0 = p * WP, nw = W - w0 < WP ? W - w0 : WP;
+      if (nw <= 0) break;
+      if (act && !trunc && w >= w0 && w < w0 + nw)  // (out + w * L lands at column (w - w0) * L)
+        build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, stg + lane * RS - w0 * L);
+      __syncthreads();
+      const int NL = nw * L, n = nenv * NL;
+      const int dq = nt / NL, dr = nt % NL;  // (env, column) step of the flat index per iteration
+      int ev = (int)threadIdx.x / NL, j = (int)threadIdx.x % NL;
+      float* dst = io.obs + e0 * WL + w0 * L;
+      for (int i = (int)threadIdx.x; i < n; i += nt) {
+        if (!Lskip[ev]) dst[(int64_t)ev * WL + j] = stg[ev * RS + j];
+        j += dr;
+        ev += dq;
+        if (j >= NL) {
+          j -= NL;
+          ev += 1;
+        }
       }
+      if (p + 1 < P) __syncthreads();  // the next phase rewrites the stage
     }
   }
   // truncation: reset the env (one sequential RNG pass per env), then every agent's reset obs
@@ -1993,8 +2001,9 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     if (c.alloc_sort) hipLaunchKernelGGL(alloc_sort_kernel, dim3(1), dim3(1024), 0, st, d, io);
     hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
   }
+  const int stage_w = c.obs_stage ? (c.W + (c.obs_stage > 1 ? c.obs_stage : 1) - 1) / (c.obs_stage > 1 ? c.obs_stage : 1) : 0;
   const size_t lds_c = (size_t)c.W * BS * sizeof(double) +
-                       (c.obs_stage ? (size_t)BS * ((c.W * c.L) | 1) * sizeof(float) + BS * sizeof(int32_t) : 0);
+                       (c.obs_stage ? (size_t)BS * ((stage_w * c.L) | 1) * sizeof(float) + BS * sizeof(int32_t) : 0);
   hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), lds_c, st, d, io);
   return hipGetLastError();
 }

@@ -35,6 +35,12 @@ def _set_alloc(monkeypatch, param):
     # runs at >= 16,384 envs, C3), on with the others (its default below that), so both forms of the
     # two phase kernels meet every reference
     monkeypatch.setenv("MSC_OBS_RING_REG", "0" if impl.startswith("lane") else "1")
+    # step_c's observation stage: the library's choice with the lane kernel (two phases; off with
+    # episode-ahead demand, as with scan), the whole block in one phase with the group kernel
+    if impl == "group":
+        monkeypatch.setenv("MSC_OBS_STAGE", "1")
+    else:
+        monkeypatch.delenv("MSC_OBS_STAGE", raising=False)
     ea = "0" if "ea0" in opts or impl.startswith("lane") else "1" if ("ea1" in opts or impl == "scan") else None
     if ea is None:
         monkeypatch.delenv("MSC_EA", raising=False)
