@@ -132,12 +132,24 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
   uint32_t stock[K];
 #pragma unroll
   for (int sk = 0; sk < K; sk++) stock[sk] = 0u;
+  // every load issued unconditionally (clamped indices, the value masked after): a load under a
+  // lane condition became a branch with its own wait, i.e. MWL * K serial round trips per launch
+  int invv[MWL][K];
+  {
+    const int64_t ec = ev ? e : 0;
+#pragma unroll
+    for (int i = 0; i < MWL; i++) {
+      const int w = gw(i), wc = w < W ? w : W - 1;
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) invv[i][sk] = gp(s.inv)[(int64_t)(wc * K + sk) * E + ec];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MWL; i++) {
     const int w = gw(i);
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
-      const int v = (ev && w < W) ? gp(s.inv)[(int64_t)(w * K + sk) * E + e] : 0;
+      const int v = (ev && w < W) ? invv[i][sk] : 0;
       Linv[(i * K + sk) * 64] = v;
       if (SH) Lshh[(i * K + sk) * 64] = 0;
       stock[sk] |= v > 0 ? (1u << i) : 0u;

@@ -1457,10 +1457,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
   auto closest_of = [&](int r) { return TAB ? lcl[r] : closest[r]; };
 
   int inv[K], qsr[K];
+  {  // unconditional loads at clamped indices (a lane-conditional load is a branch with its own wait)
+    const int64_t ec = ev ? e : 0;
+    const int wc = wl ? w : 0;
 #pragma unroll
-  for (int sk = 0; sk < K; sk++) {
-    inv[sk] = (ev && wl) ? s.inv[(int64_t)(w * K + sk) * E + e] : 0;
-    qsr[sk] = 0;
+    for (int sk = 0; sk < K; sk++) {
+      const int v = s.inv[(int64_t)(wc * K + sk) * E + ec];
+      inv[sk] = (ev && wl) ? v : 0;
+      qsr[sk] = 0;
+    }
   }
   double pen = 0.0, out = 0.0, cof = 0.0, cov = 0.0;
   // record (n, v) of this lane's env at base + n * nstep + v * vstep (uint4 units)
