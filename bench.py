@@ -30,10 +30,37 @@ sys.path.insert(0, str(REPO / "oracle"))
 
 BASELINE = json.loads((REPO / "BASELINE.json").read_text())
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
-# VALU issue peak, measured (tools/ubench_isa.hip, profiles/r02/ubench_isa.txt): independent
-# v_add_u32 at 4 waves per SIMD retire one wave64 instruction per 1.78 ns per SIMD, i.e.
-# 1024 SIMDs / 1.784 ns = 574 G wave-instructions/s (integer multiplies and f64 mul/compare: 430-500)
-VALU_PEAK_WINST = 1024 / 1.784e-9
+# VALU issue peak (MI355X_MICROARCH.md:54): a wave64 VALU instruction issues over 2 cycles on its
+# SIMD-32, so the chip issues 1024 SIMDs x clock / 2 wave-instructions per second: 1228.8 G/s at the
+# 2400 MHz max clock (MI355X_MICROARCH.md:34). Objects that know the kernel's effective clock under
+# load (rocprofv3 GRBM_GUI_ACTIVE pass, profiles/traffic.json) also quote the peak at that clock.
+CLOCK_MAX_MHZ = 2400.0
+
+
+def valu_peak(clk_mhz: float = CLOCK_MAX_MHZ) -> float:
+    return 1024 * clk_mhz * 1e6 / 2
+
+
+VALU_PEAK_WINST = valu_peak()
+# secondary, measured (tools/ubench_isa.hip, profiles/r02/ubench_isa.txt): independent v_add_u32 at
+# 4 waves per SIMD retired one wave64 instruction per 1.78 ns per SIMD = 574 G/s for the chip at the
+# (unrecorded) clock of that run; f64 mul / 64-bit mad: 1.35-1.7x the cost of a v_add_u32
+VALU_UBENCH_WINST = 1024 / 1.784e-9
+
+
+def issue_object(insts: float, seconds: float, clk_mhz=None, **extra) -> dict:
+    """VALU issue roofline: insts wave-instructions over `seconds` against the 2-cycle peak at the
+    max clock (frac) and, when known, at the kernel's effective clock (frac_at_clock)."""
+    ach = insts / seconds
+    o = dict(extra)
+    o.update({"bound": "valu issue", "achieved": round(ach / 1e9, 2), "peak": round(VALU_PEAK_WINST / 1e9, 1),
+              "unit": "G wave-instructions/s", "frac": round(ach / VALU_PEAK_WINST, 4),
+              "peak_basis": "1024 SIMDs x 2400 MHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md:34,54)",
+              "ubench_peak": round(VALU_UBENCH_WINST / 1e9, 1)})
+    if clk_mhz:
+        pk = valu_peak(clk_mhz)
+        o.update({"clock_mhz": clk_mhz, "peak_at_clock": round(pk / 1e9, 1), "frac_at_clock": round(ach / pk, 4)})
+    return o
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
 DEMAND_KERNEL = "demand_unit_kernel"
 STEP_KERNELS = ("step_a_kernel", "alloc_lane_kernel", "step_c_kernel")
@@ -191,18 +218,18 @@ def c2_line(args, rank: int):
     if tj.exists():
         tr = json.loads(tj.read_text())
         key = f"{spec.W}x{spec.R}x{spec.K}x{E}"
-        names = ("step_a_kernel", "alloc_scan_kernel", "step_c_kernel")
-        cn = [tr.get("counters", {}).get(key, {}).get(n, {}).get("SQ_INSTS_VALU") for n in names]
+        cs = tr.get("counters", {}).get(key, {})
+        names = tuple(n for n in cs if n not in (DEMAND_KERNEL, DEMAND_KERNEL + "_ea", "reset_kernel",
+                                                 "ea_materialize_kernel")) or ("step_a_kernel", "alloc_scan_kernel", "step_c_kernel")
+        cn = [cs.get(n, {}).get("SQ_INSTS_VALU") for n in names]
         tb = [tr.get(key, {}).get(n) for n in names]
         if all(x is not None for x in cn) and tm["step_ms"] > 0:
-            ach = sum(cn) / (tm["step_ms"] * 1e-3)
-            out["roofline"] = {"kernel": "step_kernels (step_a + alloc_scan + step_c)", "bound": "valu issue",
-                               "insts_per_step": int(sum(cn)), "achieved": round(ach / 1e9, 2),
-                               "peak": round(VALU_PEAK_WINST / 1e9, 1), "unit": "G wave-instructions/s",
-                               "frac": round(ach / VALU_PEAK_WINST, 4),
-                               "traffic": sum(tb) if all(x is not None for x in tb) else None,
-                               "note": "one env per wave in the allocation (4 waves per SIMD at 4,096 envs): "
-                                       "issue-bound per SIMD, DESIGN.md section 3"}
+            out["roofline"] = issue_object(
+                sum(cn), tm["step_ms"] * 1e-3, None, kernel="step_kernels (" + " + ".join(names) + ")",
+                insts_per_step=int(sum(cn)), traffic=sum(tb) if all(x is not None for x in tb) else None,
+                note="VALU wave-instructions of the step kernels (PMC) over their live time per step; the scan "
+                     "allocation runs one env per wave (4 waves per SIMD at 4,096 envs) and is latency-bound on "
+                     "its per-order DPP / permute chain, not issue-bound (DESIGN.md section 3)")
     if args.rollout_T > 0:
         out["rollout"] = {"value": round(E * spec.W * T / t_roll, 1), "unit": "agent-steps/s",
                           "ms_per_step": round(t_roll / T * 1e3, 4), "T": T,
@@ -212,6 +239,56 @@ def c2_line(args, rank: int):
                           "includes": "env step, actor + critic forward, Gaussian sampling, buffer writes, truncation "
                                       "bootstrap, GAE kernel, adv-norm statistics + normalise"}
     env.close()
+    return out
+
+
+def c5_line(args, rank: int):
+    """BASELINE configs[4]: 16 agents x 256 regions x 5 SKUs, 8,192 envs, empirical demand traces (a
+    synthetic preprocessor frame of ~200-1,000 orders per step), excluded-region mapping shape; the
+    env step only (its MAPPO rollout is `python bench.py --config c5`)."""
+    import torch
+    from marlsc import make_synthetic_env_config
+    from marlsc.seeding import default_train_seed
+    from marlsc.spec import EnvSpec
+    from marlsc.synthetic import make_synthetic_trace
+    from marlsc.vec_env import VecInventoryEnv
+    cfg = make_synthetic_env_config(16, 256, 5)
+    cfg["components"]["demand_sampler"] = {"type": "empirical", "params": None}
+    meta = {"include_warehouse_id": True, "demand_trace": make_synthetic_trace(256, 5, 300, orders_per_step=(200, 1000), seed=0)}
+    if args.obs_norm != "off":
+        meta["obs_normalization"] = args.obs_norm
+        meta["obs_stats"] = bench_obs_stats(cfg, dict(meta))
+    spec = EnvSpec.from_config(cfg, meta)
+    E = args.c5_envs
+    env = VecInventoryEnv(None, E, spec=spec, device=torch.cuda.current_device(), base_seed=default_train_seed(42))
+    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    pool = [torch.rand((E, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
+    env.reset()
+    steps = max(100, args.steps)
+    dt, tm = time_env(env, pool, steps, args.warmup, 1)
+    env.close()
+    mean_orders = float(spec.trace["offsets"][-1]) / spec.trace["n_rows"]
+    out = {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x {spec.K} SKUs, "
+                       f"empirical demand trace ({mean_orders:.0f} orders per step on average) (BASELINE configs[4])",
+           "value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "ms_per_step": round(dt / steps * 1e3, 4),
+           "steps": steps, "warmup": args.warmup, "obs_normalization": meta.get("obs_normalization", "off"),
+           "host_ms_per_step": round(tm["host_ms_per_step"], 4),
+           "kernels_ms": {"step_kernels": round(tm["step_ms"], 4)}}
+    # the step kernels (no demand kernel: the trace window is read inside step_a) against the VALU
+    # issue peak and their HBM bytes, from the PMC passes of this workload (profiles/traffic.json)
+    tj = Path(args.traffic_json)
+    if tj.exists() and tm["step_ms"] > 0:
+        tr = json.loads(tj.read_text())
+        key = f"{spec.W}x{spec.R}x{spec.K}x{E}"
+        cs = tr.get("counters", {}).get(key, {})
+        names = tuple(n for n in cs if n not in ("reset_kernel",))
+        cn = [cs[n].get("SQ_INSTS_VALU") for n in names]
+        tb = [tr.get(key, {}).get(n) for n in names]
+        if names and all(x is not None for x in cn):
+            out["roofline"] = issue_object(
+                sum(cn), tm["step_ms"] * 1e-3, None, kernel="step_kernels (" + " + ".join(names) + ")",
+                insts_per_step=int(sum(cn)), traffic=sum(tb) if all(x is not None for x in tb) else None,
+                note="the allocation is one env per lane group on the per-order argmin chain (DESIGN.md section 3)")
     return out
 
 
@@ -264,6 +341,7 @@ def main():
     ap.add_argument("--rollout-T", type=int, default=100,
                     help="steps of the MAPPO rollout line (0 = skip): env + actor/critic forward + buffers + GAE")
     ap.add_argument("--c2-envs", type=int, default=4096, help="envs of the configs[1] line (0 = skip it)")
+    ap.add_argument("--c5-envs", type=int, default=8192, help="envs of the configs[4] line (0 = skip it)")
     ap.add_argument("--obs-norm", choices=("meanstd_custom", "off"), default="meanstd_custom",
                     help="observation normalisation of the headline env (the reference MAPPO config's is meanstd_custom)")
     ap.add_argument("--rollout-lanes", type=int, default=int(os.environ.get("MSC_ROLLOUT_LANES", "1")),
@@ -412,6 +490,9 @@ def main():
     if world == 1 and args.c2_envs > 0 and args.config == "c3":
         env.close()
         c2 = c2_line(args, rank)
+    c5 = None
+    if world == 1 and args.c5_envs > 0 and args.config == "c3":
+        c5 = c5_line(args, rank)
     tt = torch.tensor([dt, t_roll], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -433,24 +514,17 @@ def main():
         if tj.exists():
             tr = json.loads(tj.read_text())
             # the phase kernels this workload ran (allocation: lane / group (+ order sort) / scan)
-            step_names = tuple(n for n in tr.get(key, {}) if n not in (DEMAND_KERNEL, DEMAND_KERNEL + "_ea", "reset_kernel"))
+            step_names = tuple(n for n in tr.get(key, {}) if n not in (DEMAND_KERNEL, DEMAND_KERNEL + "_ea", "reset_kernel",
+                                                                        "ea_materialize_kernel"))
             names = (step_names or STEP_KERNELS) if dom == "step_kernels" else (dom,)
             tb = [tr.get(key, {}).get(n) for n in names]
             traffic = sum(tb) if all(x is not None for x in tb) else None
             cn = [tr.get("counters", {}).get(key, {}).get(n, {}).get("SQ_INSTS_VALU") for n in names]
             if all(x is not None for x in cn):
-                ach = sum(cn) / t_dom
-                valu = {"insts_per_launch": int(sum(cn)), "achieved": round(ach / 1e9, 2),
-                        "peak": round(VALU_PEAK_WINST / 1e9, 1), "unit": "G wave-instructions/s",
-                        "frac": round(ach / VALU_PEAK_WINST, 4)}
-                # the kernel's effective clock under load (GRBM_GUI_ACTIVE / 8 / wall, PMC pass): a
-                # wave64 VALU instruction takes 4 cycles of a SIMD, so the issue peak at that clock is
-                # 1024 SIMDs x clock / 4
+                # the kernel's effective clock under load (GRBM_GUI_ACTIVE / 8 / wall, PMC pass)
                 clk = [tr.get("clock_mhz", {}).get(key, {}).get(n) for n in names]
-                if len(names) == 1 and clk[0]:
-                    pk = 1024 * clk[0] * 1e6 / 4
-                    valu.update({"clock_mhz": clk[0], "peak_at_clock": round(pk / 1e9, 1),
-                                 "frac_at_clock": round(ach / pk, 4)})
+                valu = issue_object(sum(cn), t_dom, clk[0] if len(names) == 1 else None,
+                                    insts_per_launch=int(sum(cn)))
         # the whole pipelined step against the same issue peak: every kernel of a step (demand of
         # t + 1 and the step kernels of t run concurrently) over the measured time per step
         step_valu = None
@@ -459,10 +533,8 @@ def main():
             names_all = ((DEMAND_KERNEL,) if DEMAND_KERNEL in cs else ()) + (step_names or STEP_KERNELS)
             vals = [cs.get(n, {}).get("SQ_INSTS_VALU") for n in names_all]
             if all(x is not None for x in vals):
-                ach_s = sum(vals) / (dt / K)
-                step_valu = {"insts_per_step": int(sum(vals)), "kernels": list(names_all),
-                             "achieved": round(ach_s / 1e9, 2), "peak": round(VALU_PEAK_WINST / 1e9, 1),
-                             "unit": "G wave-instructions/s", "frac": round(ach_s / VALU_PEAK_WINST, 4)}
+                step_valu = issue_object(sum(vals), dt / K, None, insts_per_step=int(sum(vals)),
+                                         kernels=list(names_all))
         achieved = bytes_dom / t_dom / 1e9
         out = {
             "metric": BASELINE["metric"],
@@ -512,6 +584,8 @@ def main():
                             "buffer writes, truncation bootstrap, GAE kernel, adv-norm all-reduce + normalise"}
         if c2 is not None:
             out["c2"] = c2
+        if c5 is not None:
+            out["c5"] = c5
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
         print(json.dumps(out))

@@ -45,7 +45,7 @@ extern "C" {
 typedef struct msc_env msc_env;
 typedef struct ihipStream_t* msc_stream_t; /* == hipStream_t */
 
-#define MSC_ABI_VERSION 1
+#define MSC_ABI_VERSION 2
 #define MSC_MAX_W 16   /* warehouses (agents) per env */
 #define MSC_MAX_K 8    /* SKUs */
 #define MSC_MAX_R 4096 /* demand regions */
@@ -133,6 +133,13 @@ typedef struct msc_env_desc {
   const float* obs_mean;               /* [n_features] for MSC_OBS_MEANSTD */
   const float* obs_std;
   int32_t num_eval_episodes;           /* <= 0: no eval cycling (multi_env.py:164-168, 220-224) */
+  /* Episode-ahead Poisson demand (no reference counterpart: a scheduling choice, results are
+   * identical either way): -1 automatic (on for <= 8,192 envs), 0 off (short-lived envs, e.g. the
+   * evaluation envs), n > 0 at most n slots (future episodes per env). Its buffers take at most
+   * ea_mem_fraction (<= 0: 0.25) of the device memory free at create time; fewer slots, or none,
+   * when the budget binds (msc_env_dims reports the slots chosen). */
+  int32_t episode_ahead;
+  double ea_mem_fraction;
 } msc_env_desc;
 
 /* Optional per-step diagnostics = the reference's collect_step_info dict (multi_env.py:330-361).
@@ -162,10 +169,10 @@ int msc_env_create(const msc_env_desc* desc, int device, int64_t n_envs, uint32_
                    msc_env** out);
 void msc_env_destroy(msc_env* env);
 
-/* Sizes of the I/O tensors. */
+/* Sizes of the I/O tensors, and the episode-ahead slots per env chosen at create time (0: off). */
 int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t* n_skus,
                  int32_t* n_regions, int32_t* local_obs_dim, int32_t* n_features,
-                 int32_t* max_expected_lead_time);
+                 int32_t* max_expected_lead_time, int32_t* ea_slots);
 
 #define MSC_RESET_EVAL_RESTART 1  /* reset(seed=...) of a construction-seeded eval env: counter -> 0 */
 
@@ -222,6 +229,10 @@ int msc_env_read_timing(msc_env* env, double* demand_ms, double* step_ms, int64_
  * launches timed since msc_env_set_timing (one launch = one episode of every env in steady state),
  * their count, the slots per env (0: EA off) and whether the current episode reads a slot. */
 int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* slots, int32_t* active);
+
+/* Episode-ahead memory of the handle: the budget computed at create time (bytes; 0 when EA was not
+ * requested) and the bytes allocated for the slots (0: EA off). */
+int msc_env_ea_memory(const msc_env* env, int64_t* budget_bytes, int64_t* allocated_bytes);
 
 /* Flat per-agent observation of the reference [E][W][L*(1+W)] = local_w || local_0..local_{W-1},
  * from the compact obs [E][W][L]. */

@@ -66,6 +66,7 @@ struct msc_env {
   // running then, which keeps the per-step path). At the end of episode n its slot is refilled
   // with episode n + S. Any desynchronising event (masked reset, load_state, disabling) stops it;
   // it restarts at the next common episode start.
+  int64_t ea_budget = 0, ea_bytes = 0;  // episode-ahead memory budget and bytes allocated (create time)
   bool ea_enabled = false;  // configured: Poisson demand, few envs (or MSC_EA=1), buffers allocated
   bool ea_running = false;
   int64_t ea_n = 0;         // episode (relative to the snapshot) the envs are in
@@ -443,11 +444,13 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     // chains (MSC_EA=0|1 forces it off / on)
     c.ea_S = 0;
     if (d->demand_type == MSC_DEMAND_POISSON) {
-      bool want = n_envs <= 8192;
+      bool want = d->episode_ahead < 0 ? n_envs <= 8192 : d->episode_ahead > 0;
       if (const char* ea = getenv("MSC_EA")) want = atoi(ea) != 0;
       // 16 slots: the generation runs further ahead of the step (C2 over 48 episodes: 175.5 M
       // agent-steps/s at 12 slots, 180-183 M at 16; profiles/r03/ab_ea_slots.txt); 29 GB at 4,096 envs
+      // (the memory budget below may lower it)
       int S = 16;
+      if (d->episode_ahead > 0 && d->episode_ahead < S) S = d->episode_ahead;
       if (const char* es = getenv("MSC_EA_SLOTS")) S = atoi(es);
       S = S < 2 ? 2 : (S > MSC_EA_MAX_S ? MSC_EA_MAX_S : S);
       if (want) {
@@ -602,12 +605,32 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       sb.n_orders = (int32_t*)(base + rec_bytes);
     }
   }
+  if (c.ea_S > 0) {
+    // episode-ahead memory budget: at most ea_mem_fraction (default 0.25, MSC_EA_MEM_FRAC) of the
+    // memory free now, so the rollout / learner allocations that follow keep the rest; the slot
+    // count shrinks to what fits, and below 2 slots EA stays off
+    const int T = c.T;
+    const size_t slot_bytes = sizeof(uint4) * (size_t)nv * c.ea_cap * E + sizeof(int32_t) * (size_t)(T + 1) * E +
+                              sizeof(uint32_t) * (size_t)T * E + sizeof(int32_t) * (size_t)E;
+    double frac = d->ea_mem_fraction > 0.0 ? d->ea_mem_fraction : 0.25;
+    if (const char* mf = getenv("MSC_EA_MEM_FRAC")) frac = atof(mf);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+      (void)hipGetLastError();
+      free_b = 0;
+    }
+    const double budget = frac * (double)free_b;
+    const int64_t fit = (int64_t)(budget / (double)(slot_bytes + 1024 /* alignment slack */));
+    if (fit < c.ea_S) c.ea_S = fit < 2 ? 0 : (int)fit;
+    env->ea_budget = (int64_t)budget;
+  }
   if (c.ea_S > 0) {  // episode-ahead buffers; without the memory EA stays off
     const int S = c.ea_S, T = c.T;
     const size_t rec = sizeof(uint4) * (size_t)nv * c.ea_cap * S * E;
     const size_t offb = sizeof(int32_t) * (size_t)S * (T + 1) * E, posb = sizeof(uint32_t) * (size_t)S * T * E;
     const size_t cntb = sizeof(int32_t) * (size_t)S * E;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    env->ea_bytes = (int64_t)(al(rec) + al(offb) + al(posb) + al(cntb));
     if (hipMalloc(&env->ea_mem, al(rec) + al(offb) + al(posb) + al(cntb)) == hipSuccess) {
       char* b = (char*)env->ea_mem;
       s.ea_rec = s2.ea_rec = (uint4*)b;
@@ -638,6 +661,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     } else {
       (void)hipGetLastError();
       env->ea_mem = nullptr;
+      env->ea_bytes = 0;
       c.ea_S = 0;
     }
   }
@@ -734,8 +758,15 @@ void msc_env_destroy(msc_env* env) {
   delete env;
 }
 
+int msc_env_ea_memory(const msc_env* env, int64_t* budget_bytes, int64_t* allocated_bytes) {
+  if (!env) return set_err(-1, "null env");
+  if (budget_bytes) *budget_bytes = env->ea_budget;
+  if (allocated_bytes) *allocated_bytes = env->ea_enabled ? env->ea_bytes : 0;
+  return 0;
+}
+
 int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t* n_skus, int32_t* n_regions,
-                 int32_t* local_obs_dim, int32_t* n_features, int32_t* max_lead) {
+                 int32_t* local_obs_dim, int32_t* n_features, int32_t* max_lead, int32_t* ea_slots) {
   if (!env) return set_err(-1, "null env");
   if (n_envs) *n_envs = env->c.E;
   if (n_agents) *n_agents = env->c.W;
@@ -744,6 +775,7 @@ int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t
   if (local_obs_dim) *local_obs_dim = env->c.L;
   if (n_features) *n_features = env->c.F;
   if (max_lead) *max_lead = env->c.Lmax;
+  if (ea_slots) *ea_slots = env->ea_enabled ? env->c.ea_S : 0;
   return 0;
 }
 

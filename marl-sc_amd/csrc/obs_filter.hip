@@ -2,7 +2,7 @@
 // reference src/algorithms/mappo.py:170-171, ippo.py:173-175, evaluation with update=False at
 // base.py:131-140 / :176-177) on the device. RLlib (ray 2.52.1, requirements.txt:81) is not part of
 // the reference or of this image: the algorithm is ray.rllib.utils.filter's RunningStat /
-// MeanStdFilter as published, restated in oracle/meanstd_filter.py (parity unpinned).
+// MeanStdFilter as published, restated in oracle/meanstd_ref.py (parity unpinned).
 //
 // Per column (agent, feature) a RunningStat {n, M, S}:
 //   push(x):  n += 1; n == 1: M = x; else delta = x - M, M += delta / n, S += delta * delta * (n - 1) / n

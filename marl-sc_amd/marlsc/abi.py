@@ -10,7 +10,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_W, MAX_K, MAX_R, HISTORY = 16, 8, 4096, 5
 
 DEMAND = {"poisson": 0, "empirical": 1}
@@ -55,6 +55,7 @@ class MscEnvDesc(C.Structure):
         ("feature_flags", C.c_uint32), ("include_warehouse_id", C.c_int32),
         ("obs_norm", C.c_int32), ("obs_mean", fp), ("obs_std", fp),
         ("num_eval_episodes", C.c_int32),
+        ("episode_ahead", C.c_int32), ("ea_mem_fraction", C.c_double),
     ]
 
 
@@ -97,7 +98,8 @@ def lib() -> C.CDLL:
                                  P(C.c_uint32), P(vp)]
     L.msc_env_destroy.argtypes = [vp]
     L.msc_env_destroy.restype = None
-    L.msc_env_dims.argtypes = [vp, P(C.c_int64), ip, ip, ip, ip, ip, ip]
+    L.msc_env_ea_memory.argtypes = [vp, P(C.c_int64), P(C.c_int64)]
+    L.msc_env_dims.argtypes = [vp, P(C.c_int64), ip, ip, ip, ip, ip, ip, ip]
     L.msc_env_reset.argtypes = [vp, vp, vp, C.c_int32, vp, vp]
     L.msc_env_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, P(MscStepInfo), vp]
     L.msc_env_obs_flat.argtypes = [vp, vp, vp, vp]
@@ -151,7 +153,7 @@ def check(rc: int) -> None:
 
 
 EXPORTED_SYMBOLS = [
-    "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_timing", "msc_env_read_timing", "msc_env_read_timing_ea", "msc_env_obs_flat",
+    "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_ea_memory", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_timing", "msc_env_read_timing", "msc_env_read_timing_ea", "msc_env_obs_flat",
     "msc_env_read_state", "msc_env_state_bytes", "msc_env_save_state", "msc_env_load_state", "msc_env_check",
     "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_w3_layout", "msc_mlp3_relu_forward", "msc_mlp2_relu_forward",
     "msc_mlp3_relu_forward_sampled", "msc_mlp2_relu_forward_sampled",

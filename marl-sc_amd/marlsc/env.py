@@ -40,7 +40,7 @@ class InventoryEnvironment:
         self.spec = EnvSpec.from_config(env_config, env_meta, allow_nr_ne_nw=True)
         self._seeded_at_construction = seed is not None
         root = int(seed) if seed is not None else int.from_bytes(os.urandom(4), "little")
-        self._vec = VecInventoryEnv(None, 1, spec=self.spec, device=device, env_seeds=[root])
+        self._vec = VecInventoryEnv(None, 1, spec=self.spec, device=device, env_seeds=[root], episode_ahead=0)
         self.n_warehouses, self.n_skus, self.n_regions = self.spec.W, self.spec.K, self.spec.R
         self.episode_length = self.spec.episode_length
         self.feature_config = self.spec.features

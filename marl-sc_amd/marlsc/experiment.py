@@ -173,8 +173,11 @@ def run_single(args) -> Dict[str, Any]:
         train_ret = res.get("train/episode_return_mean")
         metrics.append({"iteration": it, "train_return": train_ret, "eval_return": res.get("eval/episode_return_mean")})
         # checkpoint_best on a strictly better train return (runner.py:290-339); every rank saves its
-        # runtime state into the same directory, rank 0 the learner state
-        if train_ret is not None and train_ret > best:
+        # runtime state into the same directory, rank 0 the learner state. The return is all-reduced
+        # (PPOTrainer._global_train_return) and rank 0's decision is broadcast, so every rank takes the
+        # same branch (the barrier and the save are collective across ranks)
+        new_best = _agree(train_ret is not None and train_ret > best, world)
+        if new_best:
             best, best_it = float(train_ret), it
             bp = out / "checkpoint_best"
             if rank == 0 and bp.exists():
@@ -201,6 +204,18 @@ def run_single(args) -> Dict[str, Any]:
         if metrics:
             save_training_metrics(out, metrics)
     return last
+
+
+def _agree(flag: bool, world: int) -> bool:
+    """Rank 0's value of `flag` on every rank."""
+    if world <= 1:
+        return bool(flag)
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.broadcast(t, src=0)
+    return bool(int(t.item()))
 
 
 def _barrier(world: int) -> None:

@@ -66,20 +66,22 @@ class MeanStdObsFilter:
         # lane state: {n, buffer n, 0, 0, M[C], S[C], buffer M[C], buffer S[C]} (msc_meanstd_filter)
         self.lanes = [torch.zeros(4 + 4 * self.C, dtype=torch.float64, device=self.device) for _ in range(int(n_lanes))]
         self.driver = torch.zeros(1 + 2 * self.C, dtype=torch.float64, device=self.device)
-        self._scratch: Dict[int, torch.Tensor] = {}
+        # filter scratch per (lane, rows): lanes run on their own HIP streams, so two lanes with the
+        # same env count must not share one segment buffer
+        self._scratch: Dict[tuple, torch.Tensor] = {}
         self._eval_state: Optional[torch.Tensor] = None
 
     # -- device calls -------------------------------------------------------------------------
-    def _scratch_for(self, rows: int) -> torch.Tensor:
-        s = self._scratch.get(rows)
+    def _scratch_for(self, lane: int, rows: int) -> torch.Tensor:
+        s = self._scratch.get((lane, rows))
         if s is None:
             n = int(abi.lib().msc_meanstd_scratch_doubles(rows, self.C))
             if n < 0:
                 raise ValueError("bad filter shape")
-            s = self._scratch[rows] = torch.empty(n, dtype=torch.float64, device=self.device)
+            s = self._scratch[(lane, rows)] = torch.empty(n, dtype=torch.float64, device=self.device)
         return s
 
-    def _call(self, state, x, out, mask, update):
+    def _call(self, state, x, out, mask, update, lane: int = -1):
         rows = x.shape[0]
         if x.dtype != torch.float32 or not x.is_contiguous() or x.numel() != rows * self.C:
             raise ValueError(f"observations must be contiguous f32 [rows, {self.C}]")
@@ -89,7 +91,7 @@ class MeanStdObsFilter:
             mask = mask.to(torch.uint8).contiguous()
             if mask.numel() != rows:
                 raise ValueError("mask must have one entry per row")
-        scratch = self._scratch_for(rows) if update else None
+        scratch = self._scratch_for(lane, rows) if update else None
         abi.check(abi.lib().msc_meanstd_filter(_vp(x), _vp(out), rows, self.C, _vp(mask), 1 if update else 0,
                                                _vp(state), _vp(scratch), self.clip, self.eps,
                                                C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
@@ -100,7 +102,7 @@ class MeanStdObsFilter:
         """Push the rows of obs (those with mask != 0) into lane `lane`'s filter and normalise
         them (in place unless `out`)."""
         return self._call(self.lanes[lane], obs.reshape(obs.shape[0], -1), None if out is None else out.reshape(obs.shape[0], -1),
-                          mask, True).view_as(obs)
+                          mask, True, lane).view_as(obs)
 
     def normalize(self, obs: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """filter(obs, update=False) with the driver's statistics (evaluation)."""

@@ -457,7 +457,8 @@ def compute_obs_statistics(env_config: Any, seed_manager, mode: str = "meanstd_c
     meta["obs_normalization"] = "off"
     meta.pop("obs_stats", None)
     spec = EnvSpec.from_config(env_config, meta)
-    env = VecInventoryEnv(None, 1, spec=spec, device=device, env_seeds=np.array([env_seed], dtype=np.uint32))
+    env = VecInventoryEnv(None, 1, spec=spec, device=device, env_seeds=np.array([env_seed], dtype=np.uint32),
+                          episode_ahead=0)
     rng = np.random.default_rng(action_seed)
     W, K, T, L = spec.W, spec.K, spec.episode_length, spec.n_features
     # samples stay on the device, [episode][step 0..T][agent][L] (agent order, the terminal observation
@@ -564,12 +565,25 @@ class PPOTrainer:
             batch["mean_old"], batch["log_std_old"] = mo, lo
         stats = self.learner.update(batch, self._full_fn(), self.timesteps)
         self.iteration += 1
-        done = list(self._completed)
+        ret_mean, n_ep = self._global_train_return()
         res = {"training_iteration": self.iteration, "num_env_steps_sampled_lifetime": self.timesteps,
-               "train/episode_return_mean": float(np.mean(done)) if done else None,
-               "train/episodes": self._n_episodes}
+               "train/episode_return_mean": ret_mean, "train/episodes": n_ep}
         res.update({f"learner/{k}": v for k, v in stats.items()})
         return res
+
+    def _global_train_return(self):
+        """(mean return of the smoothing windows of every rank, episodes completed on every rank).
+        RLlib aggregates episode metrics over all env runners; here every rank contributes its window
+        (sum, count) to one SUM all-reduce, so every rank reports -- and bases checkpoint_best on --
+        the same value (marlsc/experiment.py)."""
+        done = list(self._completed)
+        if self.world == 1:
+            return (float(np.mean(done)) if done else None), self._n_episodes
+        t = torch.tensor([float(np.sum(done)) if done else 0.0, float(len(done)), float(self._n_episodes)],
+                         dtype=torch.float64, device=self._ep_ret.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        s, c, n = t.tolist()
+        return (s / c if c > 0 else None), int(n)
 
     @torch.no_grad()
     def evaluate(self, n_episodes: Optional[int] = None, seed: Optional[int] = None) -> Dict[str, Any]:
@@ -590,7 +604,7 @@ class PPOTrainer:
         spec = EnvSpec.from_config(self.env_config, meta)
         root = self.eval_seed if seed is None else int(seed)
         env = VecInventoryEnv(None, n, spec=spec, device=self.device.index,
-                              env_seeds=np.full(n, root & 0xFFFFFFFF, dtype=np.uint32))
+                              env_seeds=np.full(n, root & 0xFFFFFFFF, dtype=np.uint32), episode_ahead=0)
         env.set_episode_counters(np.arange(n, dtype=np.int32))
         obs = env.reset()
         full_fn = self._full_fn()

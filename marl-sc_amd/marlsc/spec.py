@@ -300,4 +300,6 @@ class EnvSpec:
         d.obs_mean = arr(self.obs_mean, np.float32, C.c_float)
         d.obs_std = arr(self.obs_std, np.float32, C.c_float)
         d.num_eval_episodes = self.num_eval_episodes
+        d.episode_ahead = -1  # automatic; VecInventoryEnv(episode_ahead=...) overrides
+        d.ea_mem_fraction = 0.0
         return d

@@ -36,7 +36,8 @@ class VecInventoryEnv:
     def __init__(self, env_config: Any, n_envs: int, *, env_meta: Optional[Dict[str, Any]] = None,
                  device: int = 0, base_seed: Optional[int] = None, worker_index: int = 0,
                  env_index_offset: int = 0, env_seeds=None, allow_nr_ne_nw: bool = True,
-                 demand_trace: Any = None, spec: Optional[EnvSpec] = None):
+                 demand_trace: Any = None, spec: Optional[EnvSpec] = None,
+                 episode_ahead: Optional[int] = None, ea_mem_fraction: float = 0.0):
         self.spec = spec if spec is not None else EnvSpec.from_config(
             env_config, env_meta, allow_nr_ne_nw=allow_nr_ne_nw, demand_trace=demand_trace)
         self.n_envs = int(n_envs)
@@ -44,6 +45,11 @@ class VecInventoryEnv:
         self.base_seed = default_train_seed() if base_seed is None else int(base_seed)
         L = abi.lib()
         desc = self.spec.to_desc()
+        # episode-ahead Poisson demand (msc_env_desc.episode_ahead): None automatic, 0 off (short-lived
+        # envs: evaluation, observation statistics), n > 0 at most n slots; its memory is budgeted
+        # against the device's free memory (ea_mem_fraction, default 0.25)
+        desc.episode_ahead = -1 if episode_ahead is None else int(episode_ahead)
+        desc.ea_mem_fraction = float(ea_mem_fraction)
         seeds = None
         if env_seeds is not None:
             arr = np.ascontiguousarray(env_seeds, dtype=np.uint32)
@@ -55,8 +61,10 @@ class VecInventoryEnv:
                                        worker_index, env_index_offset, seeds, C.byref(h)))
         self._h = h
         n = C.c_int64()
-        W, K, R, Lo, F, lm = (C.c_int32() for _ in range(6))
-        abi.check(L.msc_env_dims(h, C.byref(n), C.byref(W), C.byref(K), C.byref(R), C.byref(Lo), C.byref(F), C.byref(lm)))
+        W, K, R, Lo, F, lm, eas = (C.c_int32() for _ in range(7))
+        abi.check(L.msc_env_dims(h, C.byref(n), C.byref(W), C.byref(K), C.byref(R), C.byref(Lo), C.byref(F), C.byref(lm),
+                                 C.byref(eas)))
+        self.ea_slots = eas.value
         self.W, self.K, self.R, self.L, self.F = W.value, K.value, R.value, Lo.value, F.value
         assert self.L == self.spec.local_obs_dim
         E, dev = self.n_envs, self.device
@@ -163,6 +171,12 @@ class VecInventoryEnv:
         d, s, nd, ns = C.c_double(), C.c_double(), C.c_int64(), C.c_int64()
         abi.check(abi.lib().msc_env_read_timing(self._h, C.byref(d), C.byref(s), C.byref(nd), C.byref(ns)))
         return {"demand_ms": d.value, "step_ms": s.value, "n_demand": nd.value, "n_step": ns.value}
+
+    def ea_memory(self) -> Dict[str, int]:
+        """Episode-ahead memory (msc_env_ea_memory): the create-time budget and the bytes allocated."""
+        b, a = C.c_int64(), C.c_int64()
+        abi.check(abi.lib().msc_env_ea_memory(self._h, C.byref(b), C.byref(a)))
+        return {"budget": b.value, "allocated": a.value, "slots": self.ea_slots}
 
     def read_timing_ea(self) -> Dict[str, float]:
         """Episode-ahead demand (msc_env_read_timing_ea): mean device ms of the timed episode

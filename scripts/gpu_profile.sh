@@ -4,7 +4,7 @@
 # at most 64 MiB back).
 set -u
 TAG=${TAG:-r01}
-ARGS=${ARGS:-"--steps 30 --warmup 3 --no-cpu-baseline --rollout-T 0 --c2-envs 0"}
+ARGS=${ARGS:-"--steps 30 --warmup 3 --no-cpu-baseline --rollout-T 0 --c2-envs 0 --c5-envs 0"}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 run() { timeout -k 10 400 rocprofv3 "$@" -- python bench.py $ARGS > /dev/null 2>&1; }

@@ -3,7 +3,16 @@ HBM traffic of the env kernels to gpurun_out/traffic_<tag>.json.
 
 traffic = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): MI355X_MICROARCH.md "HBM [CDNA4]" -- on gfx950
 FETCH_SIZE reports half the bytes of wide coalesced reads (TCC_EA0_RDREQ x 64 B), WRITE_SIZE is
-exact for 16-B-per-lane stores."""
+exact for 16-B-per-lane stores.
+
+Only the workload's dispatches count. bench.py also runs small helper envs (observation statistics
+on one env) whose kernels share base names -- and sometimes template instantiations -- with the
+workload's, so dispatches are grouped by (kernel, grid size) and a group belongs to the workload
+only if its grid has at least E threads (E = the workload key's env count: every per-env kernel
+launches >= 1 thread per env; the one-block order-count sort is the exception). Each base name
+(template arguments stripped; the episode-ahead demand instantiation kept apart as *_ea) must then
+map to exactly one (instantiation, grid), which is what traffic_merge.py keys the JSON by.
+Usage: pmc_summary.py <tag> <workload key WxRxKxE>"""
 import collections
 import csv
 import glob
@@ -13,53 +22,69 @@ import sys
 
 tag = sys.argv[1]
 workload = sys.argv[2] if len(sys.argv) > 2 else "8x64x5x32768"
-out = collections.defaultdict(dict)
-# dispatches are grouped by kernel and grid size; per kernel only the largest grid (the workload's
-# launches, not those of the small helper envs bench.py builds, e.g. for observation statistics)
-grids = collections.defaultdict(set)
+E = int(workload.split("x")[-1])
+
+
+def base_name(full: str) -> str:
+    m = re.search(r"msc::(\w+)(?:<(.*)>)?", full)
+    if not m:
+        return ""
+    name = m.group(1)
+    if name == "demand_unit_kernel" and (m.group(2) or "").replace(" ", "").endswith(",true"):
+        name += "_ea"
+    return name
+
+
+def workload_grid(name: str, grid: int) -> bool:
+    return grid >= E or "alloc_sort_kernel" in name
+
+
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in glob.glob(f"gpurun_out/pmc_*_{tag}/**/*counter_collection.csv", recursive=True):
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for row in csv.DictReader(open(path)):
         name = row["Kernel_Name"].split("(")[0]
         grid = int(float(row.get("Grid_Size", 0) or 0))
-        grids[name].add(grid)
-        acc[(name, grid)][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    for (name, grid), v in acc.items():
-        if grid != max(grids[name]):
+        if "msc::" not in name or not workload_grid(name, grid):
             continue
-        for c, x in v.items():
-            out[name][c] = sum(x) / len(x)
-        out[name]["grid_size"] = grid
-traffic = {}
-counters = {}
-for k, v in sorted(out.items()):
-    if "msc::" not in k:
-        continue
-    print(k)
-    for c in sorted(v):
-        print(f"   {c:24s} {v[c]:.6g}")
-    m = re.search(r"msc::(\w+)", k)
-    if m and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-        traffic[m.group(1)] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
-        print(f"   => HBM traffic per launch {traffic[m.group(1)] / 1e6:.2f} MB (2 x FETCH + WRITE)")
-    if m:
-        counters[m.group(1)] = {c: v[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES") if c in v}
-# effective shader clock per kernel: GRBM_GUI_ACTIVE counts busy cycles summed over the 8 XCDs
-# (MI355X_MICROARCH.md), divided by the kernel's mean duration at the same grid (kernel trace)
-clocks = {}
+        acc[(name, grid)][row["Counter_Name"]].append(float(row["Counter_Value"]))
+# one (instantiation, grid) per base name: the largest grid (a warning if several qualify)
+chosen = {}
+for (name, grid) in acc:
+    b = base_name(name)
+    if b in chosen and chosen[b] != (name, grid):
+        print(f"# warning: {b}: several workload-sized groups {chosen[b]} / {(name, grid)}; keeping the larger grid",
+              file=sys.stderr)
+        if grid <= chosen[b][1]:
+            continue
+    chosen[b] = (name, grid)
+traffic, counters, clocks = {}, {}, {}
 dur = {}
 try:
     for row in csv.DictReader(open(f"gpurun_out/kernel_stats_by_grid_{tag}.csv")):
         name = row["Name"].split("(")[0]
         g = int(row["Grid_Size"])
-        if name not in dur or g > dur[name][0]:
-            dur[name] = (g, float(row["AverageNs"]))
+        if (name, g) in acc:
+            dur[(name, g)] = float(row["AverageNs"])
 except FileNotFoundError:
     pass
-for k, v in out.items():
-    m = re.search(r"msc::(\w+)", k)
-    if m and "GRBM_GUI_ACTIVE" in v and k in dur and dur[k][1] > 0:
-        clocks[m.group(1)] = round(v["GRBM_GUI_ACTIVE"] / 8 / dur[k][1] * 1e3, 1)  # MHz
-        print(f"{k}: effective clock {clocks[m.group(1)]} MHz (GRBM_GUI_ACTIVE / 8 / {dur[k][1] / 1e3:.1f} us)")
+for b, (name, grid) in sorted(chosen.items()):
+    v = {c: sum(x) / len(x) for c, x in acc[(name, grid)].items()}
+    v["grid_size"] = grid
+    print(f"{name}")
+    for c in sorted(v):
+        print(f"   {c:24s} {v[c]:.6g}")
+    if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+        traffic[b] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
+        print(f"   => HBM traffic per launch {traffic[b] / 1e6:.2f} MB (2 x FETCH + WRITE)")
+    counters[b] = {c: v[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES",
+                                     "SQ_LDS_BANK_CONFLICT", "grid_size") if c in v}
+    # effective shader clock: GRBM_GUI_ACTIVE counts busy cycles summed over the 8 XCDs
+    # (MI355X_MICROARCH.md), divided by the kernel's mean duration at the same grid (kernel trace)
+    d = dur.get((name, grid), 0.0)
+    if "GRBM_GUI_ACTIVE" in v and d > 0:
+        clocks[b] = round(v["GRBM_GUI_ACTIVE"] / 8 / d * 1e3, 1)  # MHz
+        print(f"{name}: effective clock {clocks[b]} MHz (GRBM_GUI_ACTIVE / 8 / {d / 1e3:.1f} us)")
+    if d > 0:
+        counters[b]["mean_ns"] = d
 json.dump({workload: traffic, "counters": {workload: counters}, "clock_mhz": {workload: clocks}},
           open(f"gpurun_out/traffic_{tag}.json", "w"), indent=1)

@@ -413,21 +413,17 @@ def test_shared_home_regions_vs_oracle(lost):
     _lockstep(spec, 192, 25, seed=8, check_every=4)
 
 
-def test_home_features_and_group_allocator_agree():
+def test_home_features_and_group_allocator_agree(monkeypatch):
     # the lane-per-env allocator (default) and the group-per-env one (MSC_ALLOC_IMPL=group) on the
     # bench shape with every home-region feature observed, against the oracle
-    import os
     feats = dict(FEATURE_CONFIG_YAML, units_shipped_home=True, incoming_demand_home=True,
                  units_shipped_away=True, stockout=True)
     cfg = make_synthetic_env_config(8, 64, 5, episode_length=30, features=feats)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
-    os.environ["MSC_ALLOC_IMPL"] = "lane"
+    monkeypatch.setenv("MSC_ALLOC_IMPL", "lane")
     _lockstep(spec, 128, 12, seed=9, check_every=3)
-    os.environ["MSC_ALLOC_IMPL"] = "group"
-    try:
-        _lockstep(spec, 128, 12, seed=9, check_every=3)
-    finally:
-        del os.environ["MSC_ALLOC_IMPL"]
+    monkeypatch.setenv("MSC_ALLOC_IMPL", "group")
+    _lockstep(spec, 128, 12, seed=9, check_every=3)
 
 
 def test_gae_vectorised_equals_scalar():
@@ -530,6 +526,45 @@ def test_episode_ahead_equals_sequential(monkeypatch, slots, batch, chunk):
     assert seen_active
     tm = a.read_timing_ea()
     assert tm["slots"] == slots and tm["n_ea"] > 0 and tm["ea_ms"] > 0
+    a.check()
+    b.check()
+
+
+def test_episode_ahead_memory_budget_binds_and_stays_exact(monkeypatch):
+    # the episode-ahead buffers take at most ea_mem_fraction of the free device
+    # memory; here the budget holds ~3.5 slots, so the handle runs with 3 slots (reported by
+    # msc_env_dims), allocates within the budget, and stays bit-exact with per-step demand
+    monkeypatch.delenv("MSC_EA", raising=False)
+    monkeypatch.delenv("MSC_EA_SLOTS", raising=False)
+    monkeypatch.setenv("MSC_ALLOC_IMPL", "scan")
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=6)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    E = 192
+    m = float(spec.lambda_orders.sum()) * 6
+    cap = int(np.ceil(m + 12.0 * np.sqrt(m + 1.0) + 64.0))
+    slot_bytes = 16 * cap * E + 4 * 7 * E + 4 * 6 * E + 4 * E
+    free, _ = torch.cuda.mem_get_info()
+    a = _vec(spec, E, base_seed=31, ea_mem_fraction=3.5 * (slot_bytes + 1024) / free)
+    b = _vec(spec, E, base_seed=31, episode_ahead=0)
+    mem = a.ea_memory()
+    assert b.ea_slots == 0 and b.ea_memory()["allocated"] == 0
+    assert a.ea_slots in (2, 3), mem
+    assert 0 < mem["allocated"] <= mem["budget"], mem
+    b.set_pipelining(False)
+    a.reset(), b.reset()
+    rng = np.random.default_rng(5)
+    seen_active = False
+    for t in range(60):
+        act = torch.from_numpy(rng.uniform(-1, 1, (E, 8, 5)).astype(np.float32)).cuda()
+        oa = a.step(act)[0].clone()
+        ob = b.step(act)[0].clone()
+        assert torch.equal(oa, ob), f"step {t}"
+        assert torch.equal(a.rewards, b.rewards), f"step {t}"
+        seen_active |= a.read_timing_ea()["active"]
+    sa, sb = a.read_state(), b.read_state()
+    for k in ("rng", "inventory", "timestep", "episode_counter"):
+        assert np.array_equal(sa[k], sb[k]), k
+    assert seen_active
     a.check()
     b.check()
 

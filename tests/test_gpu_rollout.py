@@ -107,6 +107,44 @@ def test_two_lane_rollout_matches_one_env_per_lane():
     torch.testing.assert_close(v5, col.values[5], rtol=1e-5, atol=1e-5)
 
 
+def test_two_lane_meanstd_filter_on_streams_equals_serial_lanes():
+    # two lanes with the same env count run their meanstd filter calls on their own HIP
+    # streams; each lane has its own scratch, so the concurrent run equals the same two lanes run one
+    # after the other on one stream (filter statistics and normalised observations bit-exact)
+    from marlsc import make_synthetic_env_config
+    from marlsc.rollout import ActorCritic, RolloutCollector, RolloutConfig
+    from marlsc.spec import EnvSpec
+    from marlsc.vec_env import VecInventoryEnv
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=7)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    E, T = 4096, 9
+    torch.manual_seed(0)
+    m = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, RolloutConfig()).cuda()
+
+    def run(serial):
+        lanes = [VecInventoryEnv(None, E // 2, spec=spec, device=0, base_seed=77, env_index_offset=j * E // 2)
+                 for j in range(2)]
+        for x in lanes:
+            x.reset()
+        col = RolloutCollector(lanes, m, T, seed=3, obs_filter="meanstd")
+        if serial:
+            for ln in col._lanes:
+                ln.stream = None
+        col.collect(normalize=False)
+        col.collect(normalize=False)
+        torch.cuda.synchronize()
+        out = (col.obs.clone(), col.obs_filter.driver.clone(), [s.clone() for s in col.obs_filter.lanes])
+        for x in lanes:
+            x.close()
+        return out
+
+    o1, d1, l1 = run(False)
+    o2, d2, l2 = run(True)
+    assert torch.equal(o1, o2)
+    assert torch.equal(d1, d2)
+    assert all(torch.equal(a, b) for a, b in zip(l1, l2))
+
+
 def test_fused_linear_relu_inference_matches_layer_sequence():
     # rollout inference runs Linear -> ReLU pairs as one GEMM with a ReLU epilogue; the plain layer
     # sequence (autograd path, used by the learner) must agree to GEMM rounding
