@@ -424,7 +424,7 @@ def main():
             for x in renv:
                 x.set_pipelining(os.environ.get("MSC_ROLLOUT_PIPELINE", "1") != "0")
                 x.reset()
-        t_roll = time_rollout(renv, module, args.rollout_T, world, seed=rank)
+        t_roll = time_rollout(renv, module, args.rollout_T, world, seed=0)
     # (4) the HBM-bound kernel of the rollout: msc_gae (GAE reverse scan + advantage statistics) over
     #     one MAPPO rollout's [T, E * W] sequences, timed alone with events on its stream
     gae_line = None

@@ -299,6 +299,13 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
                         const float* eps, int64_t n_rows, int32_t k, float* actions, float* logp,
                         float* clipped, msc_stream_t stream);
 
+/* Standard-normal rollout noise keyed by global env id (no reference counterpart: RLlib draws it from
+ * torch's global generator per env runner). out [n_steps][n_rows][row_len] f32: element (s, row, j)
+ * depends only on (seed, row0 + row, step0 + s, j) -- Philox4x32-10, Box-Muller -- so the noise of a
+ * global env is the same whichever rank owns it and however the envs are sharded. */
+int msc_normal_keyed(float* out, int32_t n_steps, int64_t n_rows, int32_t row_len, int64_t row0, uint64_t seed,
+                     uint64_t step0, msc_stream_t stream);
+
 /* RLlib's MeanStdFilter env-to-module connector (obs_normalization "meanstd", the reference's
  * src/algorithms/mappo.py:170-171 / ippo.py:173-175; evaluation applies it with update=False,
  * base.py:131-140, :176-177), one RunningStat per column (agent x feature) of obs [n_rows][n_cols]:

@@ -387,7 +387,9 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   {
     // A/B knobs (timing experiments only; results are identical)
     const char* impl = getenv("MSC_DEMAND_IMPL");
-    c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : 0;
+    // default (0): the split parser (demand_ab_kernel) for equal sampler parameters, the
+    // unit-per-round parser otherwise; "unit" forces the latter, "park4" the round-1 parser
+    c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : impl && strcmp(impl, "unit") == 0 ? 6 : 0;
     const char* gen = getenv("MSC_DEMAND_GEN");
     c.demand_gen = gen && atoi(gen) >= 1 && atoi(gen) <= 3 ? atoi(gen) : 3;
     const char* v = getenv("MSC_DEMAND_EPW");
@@ -1122,6 +1124,15 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
     return set_err(-1, "bad shape (n_rows %lld, k %d, log_std_rows %d)", (long long)n_rows, k, log_std_rows);
   HIP_TRY(launch_gauss_sample(mean, log_std, log_std_rows, logstd_floor, eps, n_rows, k, actions, logp, clipped,
                               (hipStream_t)stream));
+  return 0;
+}
+
+int msc_normal_keyed(float* out, int32_t n_steps, int64_t n_rows, int32_t row_len, int64_t row0, uint64_t seed,
+                     uint64_t step0, msc_stream_t stream) {
+  if (!out) return set_err(-1, "null argument");
+  if (n_steps < 0 || n_rows < 0 || row_len < 1 || row0 < 0)
+    return set_err(-1, "bad shape (n_steps %d, n_rows %lld, row_len %d)", n_steps, (long long)n_rows, row_len);
+  HIP_TRY(launch_normal_keyed(out, n_steps, n_rows, row_len, row0, seed, step0, (hipStream_t)stream));
   return 0;
 }
 

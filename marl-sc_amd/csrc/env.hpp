@@ -198,6 +198,9 @@ constexpr int SORT_BUCKETS = 1024;
 hipError_t launch_alloc_lane(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
 hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hipStream_t st);
 size_t demand_lds_bytes(const EnvConst& c);  // per block of the production demand kernel
+// demand_ab.hip: the split-parser Poisson demand kernel (equal sampler parameters in every region)
+bool demand_ab_supported(const EnvConst& c);
+hipError_t launch_demand_ab(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea);
 int order_record_vec4(int K);
 // gae.hip
 hipError_t launch_gae(const float* r, const float* v, const float* nv, const uint8_t* term, const uint8_t* trunc,
@@ -222,6 +225,8 @@ hipError_t launch_mlp2_relu(const float* x, int64_t n, int L, int H1, int KO, co
                             const float* w3p, const float* b3, float* out, const float* pre1, int grp, hipStream_t st,
                             const MlpSample* smp = nullptr);
 bool mlp2_supported(int H1);
+hipError_t launch_normal_keyed(float* out, int32_t n_steps, int64_t n_rows, int32_t row_len, int64_t row0,
+                               uint64_t seed, uint64_t step0, hipStream_t st);
 hipError_t launch_meanstd_filter(const float* x, float* out, int64_t E, int32_t C, const uint8_t* mask, int32_t update,
                                  double* state, double* scratch, double clip, double eps, hipStream_t st);
 int64_t meanstd_scratch_doubles(int64_t E, int32_t C);

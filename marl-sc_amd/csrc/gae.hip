@@ -288,4 +288,60 @@ hipError_t launch_gauss_sample(const float* mean, const float* log_std, int32_t 
   return hipGetLastError();
 }
 
+// Rollout noise keyed by global env id: out[s][row][j] = N(0, 1) from Philox4x32-10 with key =
+// seed and counter = {j / 2, global row (= row0 + row, 64 bit), step0 + s}, Box-Muller on two 32-bit
+// uniforms giving elements j (cos) and j + 1 (sin). Every value depends only on (seed, global env id,
+// rollout step, element), so a rank's envs draw the same noise whatever the sharding (the multi-rank
+// training path equals the single-rank one, tests/test_gpu_train.py).
+__device__ __forceinline__ void philox_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t h0 = __umulhi(M0, c[0]), l0 = M0 * c[0];
+  const uint32_t h1 = __umulhi(M1, c[2]), l1 = M1 * c[2];
+  const uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
+  c[0] = n0;
+  c[1] = l1;
+  c[2] = n2;
+  c[3] = l0;
+}
+
+__global__ __launch_bounds__(256) void normal_keyed_kernel(float* __restrict__ out, int32_t n_steps, int64_t n_rows,
+                                                           int32_t row_len, int64_t row0, uint64_t seed,
+                                                           uint64_t step0) {
+  const int pairs = (row_len + 1) / 2;
+  const int64_t total = (int64_t)n_steps * n_rows * pairs;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int jp = (int)(i % pairs);
+    const int64_t sr = i / pairs;
+    const int64_t row = sr % n_rows;
+    const int64_t st = sr / n_rows;
+    const uint64_t g = (uint64_t)(row0 + row);
+    uint32_t c[4] = {(uint32_t)jp, (uint32_t)g, (uint32_t)(g >> 32), (uint32_t)(step0 + (uint64_t)st)};
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+      philox_round(c, k0, k1);
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const float u1 = ((float)c[0] + 0.5f) * 2.3283064365386963e-10f;  // (0, 1]
+    const float u2 = (float)c[1] * 2.3283064365386963e-10f;
+    const float rad = sqrtf(-2.0f * logf(u1));
+    float sn, cs;
+    sincosf(6.283185307179586f * u2, &sn, &cs);
+    float* o = out + (st * n_rows + row) * row_len + 2 * jp;
+    o[0] = rad * cs;
+    if (2 * jp + 1 < row_len) o[1] = rad * sn;
+  }
+}
+
+hipError_t launch_normal_keyed(float* out, int32_t n_steps, int64_t n_rows, int32_t row_len, int64_t row0,
+                               uint64_t seed, uint64_t step0, hipStream_t st) {
+  const int64_t total = (int64_t)n_steps * n_rows * ((row_len + 1) / 2);
+  if (total == 0) return hipSuccess;
+  const int64_t blocks = (total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384;
+  hipLaunchKernelGGL(normal_keyed_kernel, dim3((unsigned)blocks), dim3(256), 0, st, out, n_steps, n_rows, row_len, row0,
+                     seed, step0);
+  return hipGetLastError();
+}
+
 }  // namespace msc

@@ -520,7 +520,8 @@ class PPOTrainer:
         self.learner = PPOLearner(self.module, cfg, seed=self.train_seed + self.rank)
         # advantages standardised per module (RLlib's GAE connector): one group for the shared policy,
         # one per agent otherwise
-        self.collector = RolloutCollector(self.env, self.module, self.T, seed=self.train_seed + 1000 + self.rank,
+        # one noise seed for every rank: the noise is keyed by global env id (msc_normal_keyed)
+        self.collector = RolloutCollector(self.env, self.module, self.T, seed=self.train_seed + 1000,
                                           adv_groups=1 if cfg.parameter_sharing else W,
                                           obs_filter="meanstd" if cfg.obs_normalization == "meanstd" else "off")
         self.env.reset()
@@ -646,7 +647,7 @@ class PPOTrainer:
         blob = self.env.save_state()
         torch.save({"env_state": torch.frombuffer(bytearray(blob), dtype=torch.uint8),
                     "obs": self.env.obs.detach().cpu(), "t_sync": int(getattr(self.env, "_t_sync", -1)),
-                    "rollout_gen": self.collector._gen.get_state(), "learner_gen": self.learner.gen.get_state(),
+                    "noise_step": int(self.collector.noise_step), "learner_gen": self.learner.gen.get_state(),
                     "ep_ret": self._ep_ret.detach().cpu(), "completed": list(self._completed),
                     "n_episodes": self._n_episodes,
                     "obs_filtered": [bool(ln.obs_filtered) for ln in self.collector._lanes]},
@@ -693,7 +694,8 @@ class PPOTrainer:
         self.env.load_state(bytes(rt["env_state"].numpy().tobytes()))
         self.env.obs.copy_(rt["obs"].to(self.device))
         self.env._t_sync = int(rt["t_sync"])
-        self.collector._gen.set_state(rt["rollout_gen"])
+        if "noise_step" in rt:  # (round <= 3 checkpoints held a per-rank torch generator instead)
+            self.collector.noise_step = int(rt["noise_step"])
         self.learner.gen.set_state(rt["learner_gen"])
         self._ep_ret.copy_(rt["ep_ret"].to(self.device))
         self._completed = deque((float(x) for x in rt["completed"]), maxlen=self._completed.maxlen)

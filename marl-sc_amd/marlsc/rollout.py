@@ -261,6 +261,19 @@ def normalize_advantages(adv: torch.Tensor, stats: torch.Tensor) -> torch.Tensor
 NOISE_CHUNK = 16  # rollout steps whose Gaussian noise is drawn in one launch
 
 
+def keyed_normal(shape, row0: int, seed: int, step0: int) -> torch.Tensor:
+    """msc_normal_keyed: f32 standard normals of shape [n_steps, n_envs, ...] on the current stream;
+    element (s, e, j) depends only on (seed, global env row0 + e, step step0 + s, flat index j)."""
+    n_steps, n_rows = int(shape[0]), int(shape[1])
+    row_len = 1
+    for d in shape[2:]:
+        row_len *= int(d)
+    out = torch.empty(tuple(shape), dtype=torch.float32, device=torch.device("cuda", torch.cuda.current_device()))
+    abi.check(abi.lib().msc_normal_keyed(_vp(out), n_steps, n_rows, row_len, int(row0), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                         int(step0), C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    return out
+
+
 class _Lane:
     """One env handle of a collector: its slice [e0, e1) of the buffers' env axis and the HIP stream
     its step chain (policy forward -> sampling -> env step) is issued on (None: the caller's)."""
@@ -284,7 +297,7 @@ class RolloutCollector:
     halves of a rank's envs: each lane's step chain runs on its own HIP stream, so one lane's env
     kernels (VALU-bound) overlap the other lane's policy GEMMs (MFMA-bound). The buffers' env axis
     is the concatenation of the lanes; each env's trajectory is the same as with one handle (envs
-    are independent and seeded by global id), the Gaussian noise differs (drawn per lane)."""
+    are independent and seeded by global id), and so is its Gaussian noise (keyed by global env id)."""
 
     def __init__(self, env, module: ActorCritic, T: int, *, seed: int = 0, adv_groups: int = 1,
                  obs_filter: str = "off"):
@@ -324,7 +337,10 @@ class RolloutCollector:
         # lane's flat buffer, which the next step rewrites. MSC_ROLLOUT_CRITIC_SIDE=0|1 forces it.
         cs = os.environ.get("MSC_ROLLOUT_CRITIC_SIDE")
         self._critic_side = (self.N <= 65536 if cs is None else cs != "0") and not self._need_flat
-        self._gen = torch.Generator(device=dev).manual_seed(seed)
+        # Gaussian action noise keyed by (seed, global env id, rollout step): msc_normal_keyed, so an
+        # env's noise does not depend on which rank or lane steps it
+        self._noise_seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.noise_step = 0  # rollout steps drawn so far (checkpointed)
         import inspect
         self._values_out = "out" in inspect.signature(module.values).parameters
         self._ls: Optional[torch.Tensor] = None
@@ -370,10 +386,11 @@ class RolloutCollector:
         if self._critic_side:
             self._critic_on_side(ln, t, sl, obs, full)
         # standard-normal noise for NOISE_CHUNK steps of the lane at once (one launch instead of one
-        # per step)
+        # per step), keyed by global env id
         if t % NOISE_CHUNK == 0:
             n = min(NOISE_CHUNK, self.T - t)
-            ln.noise = torch.randn((n,) + tuple(self.actions[t, sl].shape), device=obs.device, generator=self._gen)
+            ln.noise = keyed_normal((n,) + tuple(self.actions[t, sl].shape), ln.env.env_index_offset,
+                                    self._noise_seed, self.noise_step + t)
         eps = ln.noise[t % NOISE_CHUNK]
         a = None
         if self._ls is not None and hasattr(m, "actor_sample"):
@@ -444,6 +461,7 @@ class RolloutCollector:
                 main.wait_stream(ln.stream)
             if ln.critic_stream is not None:
                 main.wait_stream(ln.critic_stream)
+        self.noise_step += T
         # the per-env truncation flags of every step to every agent's sequence (one launch)
         self.truncated.copy_(self._trunc_env.unsqueeze(-1).expand_as(self.truncated))
         if self.obs_filter is not None:

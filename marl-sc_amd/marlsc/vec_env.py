@@ -41,6 +41,7 @@ class VecInventoryEnv:
         self.spec = spec if spec is not None else EnvSpec.from_config(
             env_config, env_meta, allow_nr_ne_nw=allow_nr_ne_nw, demand_trace=demand_trace)
         self.n_envs = int(n_envs)
+        self.env_index_offset = int(env_index_offset)  # global id of env 0 (keys the rollout noise)
         self.device = torch.device("cuda", device)
         self.base_seed = default_train_seed() if base_seed is None else int(base_seed)
         L = abi.lib()
