@@ -380,6 +380,14 @@ int msc_mlp2_relu_forward_sampled(const float* x, int64_t n_rows, int32_t in_dim
                                   const float* pre1, int32_t pre1_group, const msc_gaussian_epilogue* sample,
                                   msc_stream_t stream);
 
+/* Utility: numpy's Generator.poisson on the device (synchronous; the env's own sampler, exposed for
+ * known-answer tests): n draws with the rates lam_host[i % n_lam] (random_poisson: multiplication
+ * method below 10, PTRS at or above, numpy/random/src/distributions/distributions.c) from the PCG64
+ * state_host[6] {state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger} (the layout of
+ * msc_env_read_state's rng); draws -> out_host [n], the final state -> state_out_host (may be NULL). */
+int msc_poisson_draws(const uint64_t* state_host, const double* lam_host, int64_t n_lam, int64_t n,
+                      int64_t* out_host, uint64_t* state_out_host);
+
 /* Utility: SeedSequence(words).generate_state(1, uint32)[0] (numpy-compatible), on the host. */
 uint32_t msc_seedseq_u32(const uint32_t* words, int32_t n_words);
 

@@ -329,6 +329,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     closest[r] = b;
   }
   std::vector<double> enlam_o(R, 1.0), p_sku(R, 0.0), p_skip(R, 0.0), enlam_q((size_t)R * K, 1.0);
+  std::vector<PtrsConst> ptrs_o(R), ptrs_q((size_t)R * K);
   int order_cap = 1;
   int nv = order_record_vec4(K);
   std::vector<uint4> trec;
@@ -337,18 +338,23 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     double lam_sum = 0.0;
     for (int r = 0; r < R; r++) {
       const double lo = d->lambda_orders[r];
-      // PositiveFloat in the reference schema (schema.py:191); >= 10 would be numpy's PTRS branch
-      if (!(lo > 0.0 && lo < 10.0)) return set_err(-1, "lambda_orders[%d]=%g: only 0 < lambda < 10 (numpy multiplication method) is supported", r, lo);
+      // PositiveFloat in the reference schema (schema.py:191); >= 10 is numpy's PTRS branch
+      if (!(lo > 0.0 && lo < 1e6)) return set_err(-1, "lambda_orders[%d]=%g: must be in (0, 1e6)", r, lo);
       enlam_o[r] = exp(-lo);
-      if (lo > 0.0 && enlam_o[r] >= 1.0) return set_err(-1, "lambda_orders[%d] too small", r);
+      ptrs_o[r] = ptrs_const_host(lo);
+      if (lo >= 10.0) c.demand_ptrs = 1;
+      if (lo > 0.0 && lo < 10.0 && enlam_o[r] >= 1.0) return set_err(-1, "lambda_orders[%d] too small", r);
       p_sku[r] = d->probability_skus[r];
       // random() draws are multiples of 2^-53: U < p <=> U < ceil53(p) <=> !(U > ceil53(p) - 2^-53)
       p_skip[r] = ldexp(ceil(ldexp(p_sku[r], 53)), -53) - 0x1p-53;
       lam_sum += lo;
       for (int s = 0; s < K; s++) {
         const double lq = d->lambda_quantity[(size_t)r * K + s];
-        if (!(lq > 0.0 && lq < 10.0)) return set_err(-1, "lambda_quantity[%d,%d]=%g: only 0 < lambda < 10 is supported", r, s, lq);
+        // quantities are stored as 16-bit record fields: rates far below 2^16
+        if (!(lq > 0.0 && lq < 20000.0)) return set_err(-1, "lambda_quantity[%d,%d]=%g: must be in (0, 20000)", r, s, lq);
         enlam_q[(size_t)r * K + s] = exp(-lq);
+        ptrs_q[(size_t)r * K + s] = ptrs_const_host(lq);
+        if (lq >= 10.0) c.demand_ptrs = 1;
       }
     }
     order_cap = (int)ceil(lam_sum + 12.0 * sqrt(lam_sum + 1.0) + 64.0);
@@ -481,6 +487,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   const size_t o_ps = tp.add(p_sku.data(), sizeof(double) * R);
   const size_t o_pk = tp.add(p_skip.data(), sizeof(double) * R);
   const size_t o_elq = tp.add(enlam_q.data(), sizeof(double) * enlam_q.size());
+  const size_t o_pto = tp.add(ptrs_o.data(), sizeof(PtrsConst) * ptrs_o.size());
+  const size_t o_ptq = tp.add(ptrs_q.data(), sizeof(PtrsConst) * ptrs_q.size());
   const size_t o_elt = tp.add(d->expected_lead_times, sizeof(int32_t) * WK);
   const size_t o_md = tp.add(d->lead_type == MSC_LEAD_STOCHASTIC ? d->max_deviation : zeros_wk.data(),
                              sizeof(int32_t) * (d->lead_type == MSC_LEAD_STOCHASTIC && d->max_dev_per_sku ? K : 1));
@@ -524,6 +532,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   c.p_sku = (const double*)(tb + o_ps);
   c.p_skip = (const double*)(tb + o_pk);
   c.enlam_q = (const double*)(tb + o_elq);
+  c.ptrs_o = (const double*)(tb + o_pto);
+  c.ptrs_q = (const double*)(tb + o_ptq);
   c.elt = (const int32_t*)(tb + o_elt);
   c.maxdev = (const int32_t*)(tb + o_md);
   c.home_mask = (const uint32_t*)(tb + o_hm);
@@ -1125,6 +1135,39 @@ int msc_gaussian_sample(const float* mean, const float* log_std, int32_t log_std
   HIP_TRY(launch_gauss_sample(mean, log_std, log_std_rows, logstd_floor, eps, n_rows, k, actions, logp, clipped,
                               (hipStream_t)stream));
   return 0;
+}
+
+int msc_poisson_draws(const uint64_t* state_host, const double* lam_host, int64_t n_lam, int64_t n,
+                      int64_t* out_host, uint64_t* state_out_host) {
+  if (!state_host || !lam_host || !out_host) return set_err(-1, "null argument");
+  if (n_lam < 1 || n_lam > 4096 || n < 0) return set_err(-1, "bad shape (n_lam %lld, n %lld)", (long long)n_lam, (long long)n);
+  std::vector<PtrsConst> pc(n_lam);
+  std::vector<double> enlam(n_lam);
+  for (int64_t i = 0; i < n_lam; i++) {
+    if (!(lam_host[i] > 0.0 && lam_host[i] < 1e6)) return set_err(-1, "lam[%lld]=%g: must be in (0, 1e6)", (long long)i, lam_host[i]);
+    pc[i] = ptrs_const_host(lam_host[i]);
+    enlam[i] = exp(-lam_host[i]);
+  }
+  void* mem = nullptr;
+  const size_t b_st = 6 * sizeof(uint64_t), b_pc = sizeof(PtrsConst) * n_lam, b_el = sizeof(double) * n_lam,
+               b_out = sizeof(int64_t) * (n > 0 ? n : 1);
+  if (hipMalloc(&mem, b_st + b_pc + b_el + b_out) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(-2, "hipMalloc failed");
+  }
+  char* m = (char*)mem;
+  int rc = 0;
+  if (hipMemcpy(m, state_host, b_st, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(m + b_st, pc.data(), b_pc, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(m + b_st + b_pc, enlam.data(), b_el, hipMemcpyHostToDevice) != hipSuccess ||
+      launch_poisson_draws((uint64_t*)m, (const PtrsConst*)(m + b_st), (const double*)(m + b_st + b_pc), n_lam, n,
+                           (int64_t*)(m + b_st + b_pc + b_el), 0) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess ||
+      (n > 0 && hipMemcpy(out_host, m + b_st + b_pc + b_el, sizeof(int64_t) * n, hipMemcpyDeviceToHost) != hipSuccess) ||
+      (state_out_host && hipMemcpy(state_out_host, m, b_st, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = set_err(-2, "poisson draws: %s", hipGetErrorString(hipGetLastError()));
+  (void)hipFree(mem);
+  return rc;
 }
 
 int msc_normal_keyed(float* out, int32_t n_steps, int64_t n_rows, int32_t row_len, int64_t row0, uint64_t seed,

@@ -349,6 +349,165 @@ __global__ __launch_bounds__(BS * (2 + G)) __attribute__((amdgpu_waves_per_eu(MS
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// demand_seq_kernel: PoissonDemandSampler.sample for parameter sets with a rate >= 10 (numpy's PTRS
+// branch, demand_sampler.py:138,153 call Generator.poisson with any rate). One lane per env (or per
+// (slot, env) of an episode-ahead launch) walks the reference's loops draw by draw: a region's order
+// count, each order's K Bernoulli SKU draws, each drawn SKU's max(1, Poisson) quantity, with
+// random_poisson's branch per rate (multiplication method below 10, PTRS at or above). No generator
+// waves: PTRS trials take two draws each and reject data-dependently, which the ring parser's
+// fixed 8-draw rounds do not model; such configs are outside every BASELINE shape.
+// ------------------------------------------------------------------------------------------
+template <int K, bool EA>
+__global__ __launch_bounds__(BS) void demand_seq_kernel(const DevEnv* __restrict__ dp, EaLaunch ea) {
+  const EnvConst& c = dp->c;
+  const EnvState& s = dp->s;
+  constexpr int NV = Rec<K>::NV;
+  const int64_t E = c.E;
+  const int64_t vlane = (int64_t)blockIdx.x * BS + threadIdx.x;
+  int64_t e = vlane;
+  int slot = 0;
+  if constexpr (EA) {
+    if (vlane >= (int64_t)ea.nslots * E) return;
+    const int k = (int)(vlane / E);
+    e = vlane - (int64_t)k * E;
+    slot = (ea.slot0 + k) % c.ea_S;
+  } else if (vlane >= E) {
+    return;
+  }
+  const int cap = EA ? (int)c.ea_cap : c.order_cap;
+  const PtrsConst* pto = reinterpret_cast<const PtrsConst*>(c.ptrs_o);
+  const PtrsConst* ptq = reinterpret_cast<const PtrsConst*>(c.ptrs_q);
+  PcgCounted g{};
+  int n = 0, t_begin = 0, t_end = 1;
+  uint32_t p0 = 0;
+  if constexpr (EA) {
+    const int64_t k = vlane / E;
+    t_begin = ea.t0;
+    t_end = ea.t1;
+    uint32_t root;
+    if (ea.t0 > 0) {
+      p0 = s.ea_pos[((int64_t)slot * c.T + (ea.t0 - 1)) * E + e];
+      n = s.ea_off[((int64_t)slot * (c.T + 1) + ea.t0) * E + e];
+      const uint32_t w2[2] = {s.orig_root[e], (uint32_t)(s.ea_cnt[(int64_t)slot * E + e] - 1)};
+      root = ss_u32(w2, 2);
+    } else {
+      int cnt_new = 0;
+      root = ea_root(c, s, ea, e, (int)k, slot, cnt_new);
+      s.ea_cnt[(int64_t)slot * E + e] = cnt_new;
+      s.ea_off[(int64_t)slot * (c.T + 1) * E + e] = 0;
+    }
+    pcg_seed_child(g.r, root, 2);  // 'demand_sampler' child of the episode's root (seed_manager.py:100-120)
+    if (p0) pcg_advance(g.r, (uint64_t)p0);
+  } else {
+    g.r = load_rng(s, 0, e, E);
+    store_rng_pre(s, e, E, g.r);
+  }
+  const double* enlam_o = c.enlam_o;
+  const double* enlam_q = c.enlam_q;
+  const double* p_skip = c.p_skip;
+  for (int t = t_begin; t < t_end; t++) {
+    for (int reg = 0; reg < c.R; reg++) {
+      const int64_t no = poisson_any_g(g, enlam_o[reg], pto[reg]);
+      for (int64_t o = 0; o < no; o++) {
+        unsigned mask = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++) mask |= g.next_double() > p_skip[reg] ? 0u : (1u << k);  // U < p
+        union {
+          uint4 v[NV];
+          uint16_t h[8 * NV];
+        } u;
+#pragma unroll
+        for (int j = 0; j < 8 * NV; j++) u.h[j] = 0;
+        u.h[0] = (uint16_t)reg;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          if (mask & (1u << k)) {
+            const int64_t q = poisson_any_g(g, enlam_q[reg * K + k], ptq[reg * K + k]);
+            u.h[1 + k] = (uint16_t)(q > 1 ? q : 1);
+          }
+        }
+        n++;
+        if (n <= cap) {
+#pragma unroll
+          for (int j = 0; j < NV; j++) {
+            if constexpr (EA)
+              s.ea_rec[(((int64_t)slot * E + e) * c.ea_cap + (n - 1)) * NV + j] = u.v[j];
+            else
+              s.orders[((int64_t)(n - 1) * NV + j) * E + e] = u.v[j];
+          }
+        }
+      }
+    }
+    if constexpr (EA) {
+      s.ea_off[((int64_t)slot * (c.T + 1) + (t + 1)) * E + e] = n;
+      s.ea_pos[((int64_t)slot * c.T + t) * E + e] = p0 + g.n;
+    }
+  }
+  if (n > cap) {
+    atomicOr(s.err, ERR_ORDER_OVERFLOW);
+    n = cap;
+  }
+  if constexpr (!EA) {
+    store_rng(s, 0, e, E, g.r);
+    s.n_orders[e] = n;
+  }
+}
+
+template <int K>
+static void launch_seq_k(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea) {
+  if (ea)
+    hipLaunchKernelGGL((demand_seq_kernel<K, true>), dim3((unsigned)(((int64_t)ea->nslots * c.E + BS - 1) / BS)), dim3(BS),
+                       0, st, d, *ea);
+  else
+    hipLaunchKernelGGL((demand_seq_kernel<K, false>), dim3((unsigned)((c.E + BS - 1) / BS)), dim3(BS), 0, st, d,
+                       EaLaunch{0, 0, 0, 0, 0, 0, 0});
+}
+
+hipError_t launch_demand_seq(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea) {
+  switch (c.K) {
+    case 1: launch_seq_k<1>(c, d, st, ea); break;
+    case 2: launch_seq_k<2>(c, d, st, ea); break;
+    case 3: launch_seq_k<3>(c, d, st, ea); break;
+    case 4: launch_seq_k<4>(c, d, st, ea); break;
+    case 5: launch_seq_k<5>(c, d, st, ea); break;
+    case 6: launch_seq_k<6>(c, d, st, ea); break;
+    case 7: launch_seq_k<7>(c, d, st, ea); break;
+    case 8: launch_seq_k<8>(c, d, st, ea); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// Generator.poisson known answers on the device (msc_poisson_draws): one lane draws n variates with
+// the rates ptrs[i % n_lam] (PtrsConst + exp(-lam) per rate) from the PCG64 state[6]
+// {s_hi, s_lo, i_hi, i_lo, has32, u32} and writes the state back.
+__global__ void poisson_draws_kernel(uint64_t* state, const PtrsConst* ptrs, const double* enlam, int64_t n_lam,
+                                     int64_t n, int64_t* out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  Pcg64 r;
+  r.s_hi = state[0];
+  r.s_lo = state[1];
+  r.i_hi = state[2];
+  r.i_lo = state[3];
+  r.has32 = (uint32_t)state[4];
+  r.u32 = (uint32_t)state[5];
+  PcgRef g{r};
+  for (int64_t i = 0; i < n; i++) out[i] = poisson_any_g(g, enlam[i % n_lam], ptrs[i % n_lam]);
+  state[0] = r.s_hi;
+  state[1] = r.s_lo;
+  state[2] = r.i_hi;
+  state[3] = r.i_lo;
+  state[4] = r.has32;
+  state[5] = r.u32;
+}
+
+hipError_t launch_poisson_draws(uint64_t* state, const PtrsConst* ptrs, const double* enlam, int64_t n_lam, int64_t n,
+                                int64_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(poisson_draws_kernel, dim3(1), dim3(64), 0, st, state, ptrs, enlam, n_lam, n, out);
+  return hipGetLastError();
+}
+
 template <int K, int G>
 static void launch_ab_k(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea) {
   if (ea) {

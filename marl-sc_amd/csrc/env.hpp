@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "../../include/marlsc.h"
+#include "rng.hpp"
 
 namespace msc {
 
@@ -44,6 +45,7 @@ struct EnvConst {
   int32_t alloc_sort;   // step_b_kernel visits envs in descending order of this step's order count (perm)
   int32_t sort_shift;   // order count >> sort_shift = bucket (< SORT_BUCKETS)
   int32_t ea_S;         // episode-ahead demand: episode slots per env (0: off)
+  int32_t demand_ptrs;  // 1: some Poisson rate >= 10 (numpy's PTRS branch): the sequential sampler demand_seq_kernel
   uint32_t flags;
   int64_t E;
   int64_t ea_cap;       // episode-ahead demand: order records per (slot, env) episode
@@ -62,6 +64,8 @@ struct EnvConst {
   const MSC_G double* p_sku;       // [R]
   const MSC_G double* p_skip;      // [R]   U > p_skip[r] <=> U >= p_sku[r] (SKU not in the order), U in 2^-53 Z
   const MSC_G double* enlam_q;     // [R*K] exp(-lambda_quantity)
+  const MSC_G double* ptrs_o;      // [R][8]   PtrsConst of lambda_orders (demand_ptrs)
+  const MSC_G double* ptrs_q;      // [R*K][8] PtrsConst of lambda_quantity (demand_ptrs)
   const MSC_G int32_t* elt;        // [W*K] expected lead times
   const MSC_G int32_t* maxdev;     // [K] or [1]
   const MSC_G uint32_t* home_mask; // [R] bit w set <=> region r is warehouse w's home region
@@ -200,6 +204,9 @@ hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hip
 size_t demand_lds_bytes(const EnvConst& c);  // per block of the production demand kernel
 // demand_ab.hip: the split-parser Poisson demand kernel (equal sampler parameters in every region)
 bool demand_ab_supported(const EnvConst& c);
+hipError_t launch_demand_seq(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea);
+hipError_t launch_poisson_draws(uint64_t* state, const PtrsConst* ptrs, const double* enlam, int64_t n_lam, int64_t n,
+                                int64_t* out, hipStream_t st);
 hipError_t launch_demand_ab(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea);
 int order_record_vec4(int K);
 // gae.hip

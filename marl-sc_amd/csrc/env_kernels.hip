@@ -1845,6 +1845,10 @@ template <int K, int G>
 static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea) {
   using DFn = void (*)(const DevEnv*);
   using UFn = void (*)(const DevEnv*, EaLaunch);
+  if (c.demand_ptrs) {  // a rate >= 10: numpy's PTRS branch, the sequential sampler (demand_ab.hip)
+    launch_demand_seq(c, d, st, ea);
+    return;
+  }
   if (G == 3 && c.demand_impl == 0 && demand_ab_supported(c)) {  // the split parser (demand_ab.hip)
     launch_demand_ab(c, d, st, ea);
     return;

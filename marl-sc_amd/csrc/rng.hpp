@@ -228,6 +228,96 @@ MSC_HD int poisson_mult(Pcg64& r, double enlam) {
   }
 }
 
+// ---- random_poisson_ptrs (numpy/random/src/distributions/distributions.c, numpy 2.2): lam >= 10 --
+// Hoermann's transformed rejection. The per-rate constants come from the host libm (as numpy's own
+// computation: sqrt, log of the rate and of invalpha), laid out as 8 doubles per rate.
+struct PtrsConst {
+  double lam, slam, loglam, b, a, invalpha, vr, log_invalpha;
+};
+static_assert(sizeof(PtrsConst) == 8 * sizeof(double), "PtrsConst layout");
+inline PtrsConst ptrs_const_host(double lam) {
+  PtrsConst p;
+  p.lam = lam;
+  p.slam = sqrt(lam);
+  p.loglam = log(lam);
+  p.b = 0.931 + 2.53 * p.slam;
+  p.a = -0.059 + 0.02483 * p.b;
+  p.invalpha = 1.1239 + 1.1328 / (p.b - 3.4);
+  p.vr = 0.9277 - 3.6224 / (p.b - 2);
+  p.log_invalpha = log(p.invalpha);
+  return p;
+}
+// random_loggam (distributions.c): Stirling series with the argument shifted to >= 7
+MSC_HD double np_loggam(double x) {
+  const double a0 = 8.333333333333333e-02, a1 = -2.777777777777778e-03, a2 = 7.936507936507937e-04,
+               a3 = -5.952380952380952e-04, a4 = 8.417508417508418e-04, a5 = -1.917526917526918e-03,
+               a6 = 6.410256410256410e-03, a7 = -2.955065359477124e-02, a8 = 1.796443723688307e-01,
+               a9 = -1.39243221690590e+00;
+  if (x == 1.0 || x == 2.0) return 0.0;
+  const int64_t n = x < 7.0 ? (int64_t)(7 - x) : 0;
+  double x0 = x + (double)n;
+  const double x2 = (1.0 / x0) * (1.0 / x0);
+  double gl0 = a9;
+  gl0 *= x2; gl0 += a8;
+  gl0 *= x2; gl0 += a7;
+  gl0 *= x2; gl0 += a6;
+  gl0 *= x2; gl0 += a5;
+  gl0 *= x2; gl0 += a4;
+  gl0 *= x2; gl0 += a3;
+  gl0 *= x2; gl0 += a2;
+  gl0 *= x2; gl0 += a1;
+  gl0 *= x2; gl0 += a0;
+  double gl = gl0 / x0 + 0.5 * 1.8378770664093453e+00 + (x0 - 0.5) * log(x0) - x0;
+  for (int64_t k = 1; k <= n; k++) {
+    gl -= log(x0 - 1.0);
+    x0 -= 1.0;
+  }
+  return gl;
+}
+// the samplers below draw through a generator adaptor with next_double(): the plain stream, or one
+// that also counts the draws (the episode-ahead demand records stream positions)
+struct PcgRef {
+  Pcg64& r;
+  MSC_HD double next_double() { return pcg_double(r); }
+};
+struct PcgCounted {
+  Pcg64 r;
+  uint32_t n;
+  MSC_HD double next_double() {
+    n++;
+    return pcg_double(r);
+  }
+};
+template <class G>
+MSC_HD int64_t poisson_mult_g(G& g, double enlam) {
+  int64_t x = 0;
+  double prod = 1.0;
+  for (;;) {
+    prod *= g.next_double();
+    if (prod > enlam) x += 1;
+    else return x;
+  }
+}
+// two doubles per trial; the fast acceptance (~90 % of trials near lam = 10) needs no logarithm
+template <class G>
+MSC_HD int64_t poisson_ptrs_g(G& g, const PtrsConst& p) {
+  for (;;) {
+    const double U = g.next_double() - 0.5;
+    const double V = g.next_double();
+    const double us = 0.5 - fabs(U);
+    const int64_t k = (int64_t)floor((2 * p.a / us + p.b) * U + p.lam + 0.43);
+    if ((us >= 0.07) && (V <= p.vr)) return k;
+    if ((k < 0) || ((us < 0.013) && (V > us))) continue;
+    if ((log(V) + p.log_invalpha - log(p.a / (us * us) + p.b)) <= (-p.lam + (double)k * p.loglam - np_loggam((double)(k + 1))))
+      return k;
+  }
+}
+// random_poisson: PTRS for lam >= 10, multiplication method below (enlam = exp(-lam) from the host)
+template <class G>
+MSC_HD int64_t poisson_any_g(G& g, double enlam, const PtrsConst& p) {
+  return p.lam >= 10.0 ? poisson_ptrs_g(g, p) : poisson_mult_g(g, enlam);
+}
+
 // Generator.integers(low, high_exclusive) for ranges < 2^32 (buffered 32-bit Lemire).
 MSC_HD int64_t bounded_int(Pcg64& r, int64_t low, int64_t high_excl) {
   uint32_t rng = (uint32_t)(high_excl - 1 - low);

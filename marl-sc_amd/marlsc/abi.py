@@ -98,6 +98,7 @@ def lib() -> C.CDLL:
                                  P(C.c_uint32), P(vp)]
     L.msc_env_destroy.argtypes = [vp]
     L.msc_env_destroy.restype = None
+    L.msc_poisson_draws.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, vp]
     L.msc_normal_keyed.argtypes = [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_uint64, C.c_uint64, vp]
     L.msc_env_ea_memory.argtypes = [vp, P(C.c_int64), P(C.c_int64)]
     L.msc_env_dims.argtypes = [vp, P(C.c_int64), ip, ip, ip, ip, ip, ip, ip]
@@ -158,5 +159,5 @@ EXPORTED_SYMBOLS = [
     "msc_env_read_state", "msc_env_state_bytes", "msc_env_save_state", "msc_env_load_state", "msc_env_check",
     "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_w3_layout", "msc_mlp3_relu_forward", "msc_mlp2_relu_forward",
     "msc_mlp3_relu_forward_sampled", "msc_mlp2_relu_forward_sampled",
-    "msc_normal_keyed", "msc_meanstd_scratch_doubles", "msc_meanstd_filter", "msc_seedseq_u32", "msc_last_error", "msc_abi_version",
+    "msc_normal_keyed", "msc_poisson_draws", "msc_meanstd_scratch_doubles", "msc_meanstd_filter", "msc_seedseq_u32", "msc_last_error", "msc_abi_version",
 ]

@@ -242,8 +242,13 @@ class EnvSpec:
             raise ValueError(f"unsupported dims W={self.W} K={self.K} R={self.R} "
                              f"(max {abi.MAX_W}/{abi.MAX_K}/{abi.MAX_R})")
         if self.demand_type == "poisson":
-            if np.any(self.lambda_orders >= 10) or np.any(self.lambda_quantity >= 10):
-                raise ValueError("Poisson rates >= 10 use numpy's PTRS sampler, which is not implemented")
+            # rates >= 10 take numpy's PTRS branch (demand_sampler.py:138,153 -> Generator.poisson):
+            # the library's sequential sampler (csrc/demand_ab.hip, demand_seq_kernel)
+            if not (np.all(self.lambda_orders > 0) and np.all(self.lambda_quantity > 0)):
+                raise ValueError("Poisson rates must be positive (PositiveFloat, schema.py:191)")
+            if np.any(self.lambda_orders >= 1e6) or np.any(self.lambda_quantity >= 20000):
+                raise ValueError("Poisson rates out of range: lambda_orders < 1e6, lambda_quantity < 20000 "
+                                 "(quantities are 16-bit record fields)")
         if self.obs_mean is not None and self.obs_mean.shape != (self.n_features,):
             raise ValueError(f"obs_stats must have shape ({self.n_features},), got {self.obs_mean.shape}")
         if self.demand_type == "empirical" and self.trace["n_rows"] < self.episode_length:

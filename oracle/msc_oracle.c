@@ -125,8 +125,55 @@ static void pcg_from_pool(pcg64_t* r, const uint32_t pool[4]) {
   r->u32 = 0;
 }
 
-/* random_poisson: multiplication method for 0 < lam < 10 (lam >= 10 = PTRS, not supported). */
+/* random_loggam (numpy/random/src/distributions/distributions.c, numpy 2.2): log Gamma(x) by the
+ * Stirling series with the argument shifted to >= 7, used by the PTRS acceptance test. */
+static double np_loggam(double x) {
+  static const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03, 7.936507936507937e-04,
+                               -5.952380952380952e-04, 8.417508417508418e-04, -1.917526917526918e-03,
+                               6.410256410256410e-03, -2.955065359477124e-02, 1.796443723688307e-01,
+                               -1.39243221690590e+00};
+  if (x == 1.0 || x == 2.0) return 0.0;
+  int64_t n = x < 7.0 ? (int64_t)(7 - x) : 0;
+  double x0 = x + n;
+  const double x2 = (1.0 / x0) * (1.0 / x0);
+  const double lg2pi = 1.8378770664093453e+00;
+  double gl0 = a[9];
+  for (int k = 8; k >= 0; k--) {
+    gl0 *= x2;
+    gl0 += a[k];
+  }
+  double gl = gl0 / x0 + 0.5 * lg2pi + (x0 - 0.5) * log(x0) - x0;
+  if (x < 7.0) {
+    for (int64_t k = 1; k <= n; k++) {
+      gl -= log(x0 - 1.0);
+      x0 -= 1.0;
+    }
+  }
+  return gl;
+}
+
+/* random_poisson_ptrs (distributions.c): Hoermann's transformed rejection (Insurance: Mathematics
+ * and Economics 12, 39-45, 1993), numpy's sampler for lam >= 10; two doubles per trial. */
+static int64_t np_poisson_ptrs(pcg64_t* r, double lam) {
+  const double slam = sqrt(lam), loglam = log(lam);
+  const double b = 0.931 + 2.53 * slam;
+  const double a = -0.059 + 0.02483 * b;
+  const double invalpha = 1.1239 + 1.1328 / (b - 3.4);
+  const double vr = 0.9277 - 3.6224 / (b - 2);
+  for (;;) {
+    const double U = pcg_double(r) - 0.5;
+    const double V = pcg_double(r);
+    const double us = 0.5 - fabs(U);
+    const int64_t k = (int64_t)floor((2 * a / us + b) * U + lam + 0.43);
+    if ((us >= 0.07) && (V <= vr)) return k;
+    if ((k < 0) || ((us < 0.013) && (V > us))) continue;
+    if ((log(V) + log(invalpha) - log(a / (us * us) + b)) <= (-lam + k * loglam - np_loggam(k + 1))) return k;
+  }
+}
+
+/* random_poisson: multiplication method for 0 < lam < 10, PTRS for lam >= 10 (distributions.c). */
 static int64_t np_poisson(pcg64_t* r, double lam, double enlam) {
+  if (lam >= 10) return np_poisson_ptrs(r, lam);
   if (lam == 0) return 0;
   int64_t X = 0;
   double prod = 1.0;
@@ -193,6 +240,10 @@ void orc_rng_seed(orc_rng* r, const uint32_t* ent, int32_t n_ent, const uint32_t
 uint64_t orc_rng_next64(orc_rng* r) { uint64_t v; RNG_WRAP(v = pcg_next64(&p)); return v; }
 double orc_rng_random(orc_rng* r) { double v; RNG_WRAP(v = pcg_double(&p)); return v; }
 int64_t orc_rng_poisson(orc_rng* r, double lam) { int64_t v; RNG_WRAP(v = np_poisson(&p, lam, exp(-lam))); return v; }
+/* n draws of Generator.poisson(lam[i % n_lam]) (numpy draws an array of rates element by element) */
+void orc_rng_poisson_n(orc_rng* r, const double* lam, int64_t n_lam, int64_t n, int64_t* out) {
+  RNG_WRAP(for (int64_t i = 0; i < n; i++) out[i] = np_poisson(&p, lam[i % n_lam], exp(-lam[i % n_lam])));
+}
 int64_t orc_rng_integers(orc_rng* r, int64_t lo, int64_t hi) { int64_t v; RNG_WRAP(v = np_integers(&p, lo, hi)); return v; }
 
 /* numpy add.reduce order for a contiguous double/float vector (pairwise_sum, n <= 128 path). */

@@ -42,6 +42,7 @@ void orc_rng_seed(orc_rng* r, const uint32_t* entropy, int32_t n_entropy, const 
 uint64_t orc_rng_next64(orc_rng* r);
 double orc_rng_random(orc_rng* r);
 int64_t orc_rng_poisson(orc_rng* r, double lam);
+void orc_rng_poisson_n(orc_rng* r, const double* lam, int64_t n_lam, int64_t n, int64_t* out);
 int64_t orc_rng_integers(orc_rng* r, int64_t low, int64_t high_exclusive);
 
 #ifdef __cplusplus

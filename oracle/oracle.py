@@ -55,6 +55,8 @@ def lib():
         L.orc_rng_random.restype = C.c_double
         L.orc_rng_poisson.argtypes = [vp, C.c_double]
         L.orc_rng_poisson.restype = C.c_int64
+        L.orc_rng_poisson_n.argtypes = [vp, vp, C.c_int64, C.c_int64, vp]
+        L.orc_rng_poisson_n.restype = None
         L.orc_rng_integers.argtypes = [vp, C.c_int64, C.c_int64]
         L.orc_rng_integers.restype = C.c_int64
         _L = L
@@ -80,8 +82,22 @@ class OracleRng:
         ent, key = u32s(entropy), u32s(spawn_key) if spawn_key else None
         lib().orc_rng_seed(C.byref(self.buf), ent, len(entropy), key, len(spawn_key))
 
+    @classmethod
+    def from_state(cls, w):
+        """A stream at a raw state [state_hi, state_lo, inc_hi, inc_lo, has32, u32]."""
+        r = cls.__new__(cls)
+        r.buf = (C.c_uint64 * 6)(*[int(x) for x in np.asarray(w, dtype=np.uint64)])
+        return r
+
     def state(self):
         return np.array(list(self.buf), dtype=np.uint64)
+
+    def poisson_n(self, lam, n: int) -> np.ndarray:
+        """n draws of Generator.poisson with the rates `lam` (scalar or cycled array)."""
+        lam = np.ascontiguousarray(np.atleast_1d(lam), dtype=np.float64)
+        out = np.empty(int(n), dtype=np.int64)
+        lib().orc_rng_poisson_n(C.byref(self.buf), _ptr(lam), lam.size, int(n), _ptr(out))
+        return out
 
     def next64(self):
         return lib().orc_rng_next64(C.byref(self.buf))

@@ -579,3 +579,38 @@ def test_scan_allocator_vs_oracle_sizes(monkeypatch, E):
     cfg["components"]["demand_allocator"]["params"]["max_splits"] = 1
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     _lockstep(spec, E, 17, seed=E, check_every=2)
+
+
+def test_poisson_ptrs_device_known_answers():
+    # numpy's PTRS branch (lam >= 10) on the device (msc_poisson_draws runs the env's own sampler,
+    # rng.hpp poisson_any_g): 100,000 draws per rate and a stream cycling rates across both branches,
+    # against Generator.poisson (tests/golden/make_ptrs_vectors.py, numpy only); draws and final
+    # PCG64 states bit-exact
+    import ctypes as C
+    from pathlib import Path
+    from marlsc import abi
+    g = np.load(Path(__file__).resolve().parent / "golden" / "poisson_ptrs.npz")
+    streams = [(g[f"init_{i}"], np.array([lam]), g[f"draws_{i}"], g[f"final_{i}"]) for i, lam in enumerate(g["rates"])]
+    streams.append((g["init_mix"], g["mix_rates"], g["draws_mix"], g["final_mix"]))
+    for init, lam, draws, final in streams:
+        st = np.ascontiguousarray(init, dtype=np.uint64)
+        lam = np.ascontiguousarray(lam, dtype=np.float64)
+        out = np.empty(draws.size, dtype=np.int64)
+        fin = np.empty(6, dtype=np.uint64)
+        abi.check(abi.lib().msc_poisson_draws(st.ctypes.data_as(C.c_void_p), lam.ctypes.data_as(C.c_void_p), lam.size,
+                                              out.size, out.ctypes.data_as(C.c_void_p), fin.ctypes.data_as(C.c_void_p)))
+        bad = np.flatnonzero(out != draws.astype(np.int64))
+        assert bad.size == 0, f"lam={lam}: first mismatch at draw {bad[:5]}"
+        assert np.array_equal(fin, final)
+
+
+@pytest.mark.parametrize("ea", ["0", "1"])
+@pytest.mark.parametrize("lo,lq", [(4.0, 12.0), (11.0, 3.0)])
+def test_ptrs_rates_env_vs_oracle(monkeypatch, ea, lo, lq):
+    # Poisson rates >= 10 (numpy's PTRS branch) in the env, quantities
+    # (lambda_q = 12) or order counts (lambda_o = 11), against the oracle in lockstep, with
+    # per-step and episode-ahead demand (the sequential sampler, csrc/demand_ab.hip)
+    monkeypatch.setenv("MSC_EA", ea)
+    cfg = make_synthetic_env_config(4, 16, 3, episode_length=7, lambda_orders=lo, lambda_quantity=lq)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 96, 17, seed=4, check_every=2)

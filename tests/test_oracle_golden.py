@@ -76,3 +76,19 @@ def test_oracle_matches_reference(name):
             np.testing.assert_array_equal(st["inventory"], d["inv_after"][:, t])
             np.testing.assert_array_equal(st["rng"][:, 0], d["rng_demand"][:, t], err_msg=f"{name} t={t} rng demand")
             np.testing.assert_array_equal(st["rng"][:, 1], d["rng_lead"][:, t], err_msg=f"{name} t={t} rng lead")
+
+
+def test_poisson_ptrs_known_answers():
+    # numpy's PTRS branch (lam >= 10): 100,000 draws per rate from
+    # Generator(PCG64(SeedSequence([7, i]))).poisson and one stream cycling rates across both
+    # branches (tests/golden/make_ptrs_vectors.py, numpy only); draws and final states bit-exact
+    g = np.load(orc.HERE.parent / "tests/golden/poisson_ptrs.npz")
+    for i, lam in enumerate(g["rates"]):
+        r = orc.OracleRng.from_state(g[f"init_{i}"])
+        x = r.poisson_n(lam, g[f"draws_{i}"].size)
+        assert np.array_equal(x, g[f"draws_{i}"].astype(np.int64)), f"lam={lam}"
+        assert np.array_equal(r.state(), g[f"final_{i}"]), f"lam={lam}"
+    r = orc.OracleRng.from_state(g["init_mix"])
+    x = r.poisson_n(g["mix_rates"], g["draws_mix"].size)
+    assert np.array_equal(x, g["draws_mix"].astype(np.int64))
+    assert np.array_equal(r.state(), g["final_mix"])
