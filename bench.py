@@ -109,7 +109,7 @@ def bench_obs_stats(cfg, meta, n_episodes: int = 2):
     return compute_obs_statistics(cfg, SeedManager(42), "meanstd_custom", n_episodes=n_episodes, env_meta=meta)
 
 
-def time_env(env, pool, steps: int, warmup: int, world: int):
+def time_env(env, pool, steps: int, warmup: int, world: int, ea: bool = False):
     """warmup untimed steps, then `steps` timed ones (barrier + synchronize on both sides); then a
     timing pass of min(steps, 50) steps with the library's per-launch HIP events."""
     import torch
@@ -129,7 +129,9 @@ def time_env(env, pool, steps: int, warmup: int, world: int):
         dist.barrier()
     dt = time.perf_counter() - t0
     env.check()
-    kp = min(steps, 50)
+    # the timing pass: 50 steps, or with episode-ahead demand 2.5 episodes (a generation launch covers
+    # whole episodes of every env: one or two per episode in steady state)
+    kp = min(steps, 50) if not ea else int(2.5 * env.spec.episode_length)
     env.set_timing(kp)
     for i in range(kp):
         env.step(pool[i % len(pool)])
@@ -195,7 +197,7 @@ def c2_line(args, rank: int):
     period = 4 * T
     steps = max(6 * period, -(-args.steps // period) * period)
     warm = 6 * period
-    dt, tm = time_env(env, pool, steps, warm, 1)
+    dt, tm = time_env(env, pool, steps, warm, 1, ea=True)
     rc = RolloutConfig.from_algorithm_config(algo)
     torch.manual_seed(0)
     module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
@@ -342,6 +344,8 @@ def main():
                     help="steps of the MAPPO rollout line (0 = skip): env + actor/critic forward + buffers + GAE")
     ap.add_argument("--c2-envs", type=int, default=4096, help="envs of the configs[1] line (0 = skip it)")
     ap.add_argument("--c5-envs", type=int, default=8192, help="envs of the configs[4] line (0 = skip it)")
+    ap.add_argument("--no-ea-line", dest="ea_line", action="store_false",
+                    help="skip the episode-ahead steady-state line of the headline envs")
     ap.add_argument("--obs-norm", choices=("meanstd_custom", "off"), default="meanstd_custom",
                     help="observation normalisation of the headline env (the reference MAPPO config's is meanstd_custom)")
     ap.add_argument("--rollout-lanes", type=int, default=int(os.environ.get("MSC_ROLLOUT_LANES", "1")),
@@ -392,7 +396,13 @@ def main():
     spec = EnvSpec.from_config(cfg, meta)
     E = args.envs if args.envs is not None else (8192 if args.config == "c5" else 32768)
     dev = torch.cuda.current_device()
-    env = VecInventoryEnv(None, E, spec=spec, device=dev, base_seed=default_train_seed(42), env_index_offset=rank * E)
+    # episode-ahead buffers (the memory budget picks the slots: 4 at 32,768 envs) for the steady-state
+    # line below; the headline steps with per-step pipelined demand (EA paused)
+    want_ea = world == 1 and args.config == "c3" and args.ea_line
+    env = VecInventoryEnv(None, E, spec=spec, device=dev, base_seed=default_train_seed(42), env_index_offset=rank * E,
+                          episode_ahead=16 if want_ea else None)
+    if env.ea_slots and E > 8192:
+        env.set_episode_ahead(False)
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
     pool = [torch.rand((E, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
     env.reset()
@@ -404,6 +414,33 @@ def main():
     #     each step launch (step_a/b/c) with HIP events on the stream it runs on (msc_env_set_timing)
     dt, tm = time_env(env, pool, K, args.warmup, world)
     t_demand, t_step = tm["demand_ms"] / 1e3, tm["step_ms"] / 1e3
+    # (1b) the same envs in episode-ahead steady state: whole future episodes of
+    #      every env generated on the library's side stream while earlier ones step; a generation
+    #      launch refills one slot per episode, so the window is whole episodes after the pipeline
+    #      has filled (6 episodes of warm-up, 8 timed); every timed step's demand is generated inside
+    #      the window in steady state
+    ea_line = None
+    if want_ea and env.ea_slots:
+        T_ep = spec.episode_length
+        env.set_episode_ahead(True)
+        dt_ea, tm_ea = time_env(env, pool, 8 * T_ep, 6 * T_ep, 1, ea=True)
+        env.set_episode_ahead(False)
+        ea_line = {"value": round(E * spec.W * 8 * T_ep / dt_ea, 1), "unit": "agent-steps/s",
+                   "ms_per_step": round(dt_ea / (8 * T_ep) * 1e3, 4), "steps": 8 * T_ep, "warmup": 6 * T_ep,
+                   "slots": tm_ea["slots"], "host_ms_per_step": round(tm_ea["host_ms_per_step"], 4),
+                   "kernels_ms": {"step_kernels": round(tm_ea["step_ms"], 4),
+                                  DEMAND_KERNEL + "_ea": round(tm_ea["ea_ms"], 3),
+                                  "ea_env_steps_per_launch": int(tm_ea["ea_env_steps_per_launch"])},
+                   "note": "episode-ahead demand in steady state (msc_env_set_episode_ahead): one generation launch "
+                           "per episode refills a slot with a whole future episode of every env; the headline "
+                           "`value` is the per-step pipelined path, whose first steps the driver's short "
+                           "windows measure"}
+    # episode-ahead demand (the library's default): the demand work of the timed
+    # steps runs as generation launches of whole episodes on a side stream; per launch its duration
+    # and the env-steps it generated
+    ea_regime = tm["n_ea"] > 0 and tm["ea_env_steps_per_launch"] > 0
+    t_ea = tm["ea_ms"] / 1e3 if ea_regime else 0.0
+    ea_work = tm["ea_env_steps_per_launch"] if ea_regime else 0.0
     # (3) MAPPO rollout (configs[2]): env step + actor/critic forward + sampling + buffer writes +
     #     GAE kernel + adv-norm statistics all-reduce, T steps per rollout
     t_roll = 0.0
@@ -503,9 +540,15 @@ def main():
         mean_orders = (float(spec.trace["offsets"][-1]) / spec.trace["n_rows"] if spec.demand_type == "empirical"
                        else float(spec.lambda_orders.sum()))
         b_dem, b_step = algorithmic_bytes(spec, mean_orders)
-        kern = {DEMAND_KERNEL: (t_demand, b_dem * E), "step_kernels": (t_step, b_step * E)}
-        dom = max(kern, key=lambda k: kern[k][0])
-        t_dom, bytes_dom = kern[dom]
+        # per launch: (duration, algorithmic bytes, duration per step of the workload) -- the dominant
+        # kernel is the one with the most device time per step
+        kern = {"step_kernels": (t_step, b_step * E, t_step)}
+        if ea_regime:
+            kern[DEMAND_KERNEL + "_ea"] = (t_ea, b_dem * ea_work, t_ea * E / ea_work)
+        if t_demand > 0:
+            kern[DEMAND_KERNEL] = (t_demand, b_dem * E, t_demand)
+        dom = max(kern, key=lambda k: kern[k][2])
+        t_dom, bytes_dom, _ = kern[dom]
         # per-launch HBM bytes / instruction counts of the same workload from the rocprofv3 PMC
         # passes (scripts/gpu_profile.sh -> profiles/traffic.json)
         traffic = valu = None
@@ -530,11 +573,15 @@ def main():
         step_valu = None
         if tj.exists():
             cs = tr.get("counters", {}).get(key, {})
-            names_all = ((DEMAND_KERNEL,) if DEMAND_KERNEL in cs else ()) + (step_names or STEP_KERNELS)
+            # per step: the step kernels, plus the demand work of one step (the per-step kernel, or an
+            # episode-ahead launch's instructions scaled by E / its env-steps)
+            dname = DEMAND_KERNEL + "_ea" if ea_regime else DEMAND_KERNEL
+            dscale = E / ea_work if ea_regime else 1.0
+            names_all = ((dname,) if dname in cs else ()) + (step_names or STEP_KERNELS)
             vals = [cs.get(n, {}).get("SQ_INSTS_VALU") for n in names_all]
             if all(x is not None for x in vals):
-                step_valu = issue_object(sum(vals), dt / K, None, insts_per_step=int(sum(vals)),
-                                         kernels=list(names_all))
+                tot = sum(v * (dscale if n == dname else 1.0) for n, v in zip(names_all, vals))
+                step_valu = issue_object(tot, dt / K, None, insts_per_step=int(tot), kernels=list(names_all))
         achieved = bytes_dom / t_dom / 1e9
         out = {
             "metric": BASELINE["metric"],
@@ -558,10 +605,14 @@ def main():
                        "n_envs_per_gpu": E, "agents": spec.W, "regions": spec.R, "skus": spec.K,
                        "episode_length": spec.episode_length, "obs_dim_local": spec.local_obs_dim,
                        "obs_normalization": meta.get("obs_normalization", "off"), "parallelism": f"env-shard x{world}"},
-            "kernels_ms": {DEMAND_KERNEL: round(t_demand * 1e3, 4), "step_kernels": round(t_step * 1e3, 4)},
+            "kernels_ms": {DEMAND_KERNEL: round(t_demand * 1e3, 4), "step_kernels": round(t_step * 1e3, 4),
+                           **({DEMAND_KERNEL + "_ea": round(t_ea * 1e3, 3), "ea_env_steps_per_launch": int(ea_work),
+                               "ea_slots": tm["slots"]} if ea_regime else {})},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "bytes_per_launch": int(bytes_dom),
+                         **({"launch": f"episode-ahead generation of {int(ea_work)} env-steps (whole episodes of every env) "
+                                       f"on the library's side stream, {t_ea * 1e3:.1f} ms"} if dom.endswith("_ea") else {}),
                          "note": "not HBM-bound: the env step is VALU-issue-bound (PCG64 draws + the per-env parse and allocation chains); see valu_issue (measured issue peak) and DESIGN.md section 3"},
         }
         if valu is not None:
@@ -582,6 +633,23 @@ def main():
                 "lanes": max(1, args.rollout_lanes),
                 "includes": "env step (envs split into `lanes` handles on their own HIP streams), actor forward, MAPPO critic on local||global (first layer split: global block once per env), Gaussian sampling, "
                             "buffer writes, truncation bootstrap, GAE kernel, adv-norm all-reduce + normalise"}
+        if ea_line is not None:
+            b_dem_ea = algorithmic_bytes(spec, mean_orders)[0]
+            w_ea = ea_line["kernels_ms"]["ea_env_steps_per_launch"]
+            t_l = ea_line["kernels_ms"][DEMAND_KERNEL + "_ea"] / 1e3
+            if w_ea > 0 and t_l > 0:
+                ach = b_dem_ea * w_ea / t_l / 1e9
+                ea_line["roofline"] = {"kernel": DEMAND_KERNEL + "_ea", "bound": "hbm", "achieved": round(ach, 2),
+                                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+                                       "bytes_per_launch": int(b_dem_ea * w_ea),
+                                       "traffic": (json.loads(Path(args.traffic_json).read_text()).get(key, {})
+                                                   .get(DEMAND_KERNEL + "_ea") if Path(args.traffic_json).exists() else None)}
+                if Path(args.traffic_json).exists():
+                    ci = json.loads(Path(args.traffic_json).read_text()).get("counters", {}).get(key, {}).get(
+                        DEMAND_KERNEL + "_ea", {}).get("SQ_INSTS_VALU")
+                    if ci:
+                        ea_line["roofline"]["valu_issue"] = issue_object(ci, t_l, None, insts_per_launch=int(ci))
+            out["episode_ahead"] = ea_line
         if c2 is not None:
             out["c2"] = c2
         if c5 is not None:

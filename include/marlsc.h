@@ -203,6 +203,13 @@ int msc_env_generate_demand(msc_env* env, msc_stream_t stream);
  * way; 0 disables it (every step then runs demand + step back to back on the caller's stream). */
 int msc_env_set_pipelining(msc_env* env, int32_t enabled);
 
+/* Episode-ahead demand on / off at run time (no reference counterpart; results are identical either
+ * way): 0 switches a handle whose EA buffers exist to per-step pipelined demand from the current step
+ * on (e.g. a rollout whose policy kernels lose more to the background generation than the step
+ * gains), != 0 lets it restart at the next common episode start. No-op without EA buffers.
+ * Synchronises the device. */
+int msc_env_set_episode_ahead(msc_env* env, int32_t enabled);
+
 /* Wave priority of the step chain (no reference counterpart: a scheduling hint). With enabled != 0
  * the phase-A and phase-C kernels of msc_env_step run at s_setprio 3, like the allocation kernel,
  * ahead of the pipelined demand kernel of the next step. For callers that run their own work between
@@ -227,8 +234,10 @@ int msc_env_read_timing(msc_env* env, double* demand_ms, double* step_ms, int64_
  * src/utils/seed_manager.py:100-120, never on actions); each env step then reads its episode's
  * slot. Results are identical with and without it. Mean device duration of the episode generation
  * launches timed since msc_env_set_timing (one launch = one episode of every env in steady state),
- * their count, the slots per env (0: EA off) and whether the current episode reads a slot. */
-int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* slots, int32_t* active);
+ * their count, the slots per env (0: EA off), whether the current episode reads a slot, and the mean
+ * env-steps of demand one timed launch generated (slots x steps x envs; for roofline accounting). */
+int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* slots, int32_t* active,
+                           double* env_steps_per_launch);
 
 /* Episode-ahead memory of the handle: the budget computed at create time (bytes; 0 when EA was not
  * requested) and the bytes allocated for the slots (0: EA off). */

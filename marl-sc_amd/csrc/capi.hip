@@ -68,6 +68,8 @@ struct msc_env {
   // it restarts at the next common episode start.
   int64_t ea_budget = 0, ea_bytes = 0;  // episode-ahead memory budget and bytes allocated (create time)
   bool ea_enabled = false;  // configured: Poisson demand, few envs (or MSC_EA=1), buffers allocated
+  bool ea_paused = false;   // msc_env_set_episode_ahead(0): per-step demand until re-enabled
+  int32_t obs_stage_pe = 0, chain_prio_pe = 0;  // step_c staging / chain priority of the per-step path
   bool ea_running = false;
   int64_t ea_n = 0;         // episode (relative to the snapshot) the envs are in
   int ea_cur = -1;          // slot of the current episode, -1: per-step demand
@@ -90,6 +92,7 @@ struct msc_env {
   bool gen_pending[MSC_EA_MAX_S] = {};  // slot's generation not fully launched (ev_gen stale)
   hipEvent_t ev_gen[MSC_EA_MAX_S] = {}, ev_cons[MSC_EA_MAX_S] = {}, ev_snap = nullptr;
   std::vector<hipEvent_t> tev_ea;  // timing of EA launches (msc_env_set_timing)
+  std::vector<double> tea_work;    // env-steps generated by each timed EA launch
   int n_tea = 0;
 };
 
@@ -124,7 +127,11 @@ static int wait_ea_stream(msc_env* env, hipStream_t st) {
 static hipError_t ea_launch_chunk(msc_env* env, const EaLaunch& l) {
   hipStream_t es = env->ea_stream;
   const bool tm = env->n_tea < env->t_cap;
-  if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea], es);
+  if (tm) {
+    (void)hipEventRecord(env->tev_ea[2 * env->n_tea], es);
+    if ((int)env->tea_work.size() <= env->n_tea) env->tea_work.resize(env->n_tea + 1);
+    env->tea_work[env->n_tea] = (double)l.nslots * (double)(l.t1 - l.t0) * (double)env->c.E;
+  }
   hipError_t e = launch_demand_ea(env->c, env->dev, l, es);
   if (e != hipSuccess) return e;
   if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea++ + 1], es);
@@ -393,9 +400,9 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   {
     // A/B knobs (timing experiments only; results are identical)
     const char* impl = getenv("MSC_DEMAND_IMPL");
-    // default (0): the split parser (demand_ab_kernel) for equal sampler parameters, the
-    // unit-per-round parser otherwise; "unit" forces the latter, "park4" the round-1 parser
-    c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : impl && strcmp(impl, "unit") == 0 ? 6 : 0;
+    // default (0): the unit-per-round parser; "ab" the split chain / bookkeeper parser
+    // (demand_ab_kernel: measured slower), "park4" the round-1 parser
+    c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : impl && strcmp(impl, "ab") == 0 ? 7 : 0;
     const char* gen = getenv("MSC_DEMAND_GEN");
     c.demand_gen = gen && atoi(gen) >= 1 && atoi(gen) <= 3 ? atoi(gen) : 3;
     const char* v = getenv("MSC_DEMAND_EPW");
@@ -452,6 +459,9 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     // chains (MSC_EA=0|1 forces it off / on)
     c.ea_S = 0;
     if (d->demand_type == MSC_DEMAND_POISSON) {
+      // (automatic below 8,193 envs; at 32,768 envs it wins only in steady state -- 0.81 -> 0.72 ms
+      // per step once the generation pipeline is full, profiles/r04/ab_ea_c3.txt -- while the first
+      // episodes pay for the bulk generation, so larger handles ask for it explicitly)
       bool want = d->episode_ahead < 0 ? n_envs <= 8192 : d->episode_ahead > 0;
       if (const char* ea = getenv("MSC_EA")) want = atoi(ea) != 0;
       // 16 slots: the generation runs further ahead of the step (C2 over 48 episodes: 175.5 M
@@ -650,6 +660,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       s.ea_pos = s2.ea_pos = (uint32_t*)(b + al(rec) + al(offb));
       s.ea_cnt = s2.ea_cnt = (int32_t*)(b + al(rec) + al(offb) + al(posb));
       env->ea_enabled = true;
+      env->obs_stage_pe = c.obs_stage;
+      env->chain_prio_pe = c.chain_prio;
       // refill batch: a batch freed by episodes n-B+1 .. n is needed S-B episodes later
       int B = S / 4 > 1 ? S / 4 : 1;
       if (const char* eb = getenv("MSC_EA_BATCH")) B = atoi(eb);
@@ -667,7 +679,9 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       // chunk A/B at C2 (scripts/gpu_ab_eachunk.sh, steps per launch -> M agent-steps/s): 5 -> 149.6,
       // 10 -> 152.9, 20 -> 157.8, 34 -> 165.3, 50 -> 170.1, 100 -> 171.4 (fewer launch ramps and
       // tails beside the step kernels); 50 keeps the work a synchronize may wait for at half an episode
-      int ch = 50;
+      // at 32,768 envs whole-episode launches: 0.72 ms per step against 0.78 with 50-step chunks
+      // (profiles/r04/ab_ea_c3.txt)
+      int ch = E > 8192 ? T : 50;
       if (const char* ec = getenv("MSC_EA_CHUNK")) ch = atoi(ec);
       env->ea_chunk = ch < 1 ? 1 : ch;
     } else {
@@ -848,7 +862,7 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
   const bool poisson = c.demand_type == MSC_DEMAND_POISSON;
   const int b = (int)(env->tau & 1);
   // episode-ahead demand: start at a common episode start; an episode n >= 1 reads its slot
-  if (env->ea_enabled && env->pipeline && !env->ea_running && env->t_sync == 0)
+  if (env->ea_enabled && !env->ea_paused && env->pipeline && !env->ea_running && env->t_sync == 0)
     if (const int rc = ea_start(env, st)) return rc;
   if (env->ea_running) HIP_TRY(ea_pump(env, false));
   if (env->ea_running && env->t_sync == 0) {
@@ -919,6 +933,32 @@ int msc_env_set_pipelining(msc_env* env, int32_t enabled) {
   return 0;
 }
 
+int msc_env_set_episode_ahead(msc_env* env, int32_t enabled) {
+  if (!env) return set_err(-1, "null env");
+  if (!env->ea_enabled) return 0;  // not configured at create (or no memory): nothing to switch
+  const bool pause = enabled == 0;
+  if (pause == env->ea_paused) return 0;
+  HIP_TRY(hipSetDevice(env->device));
+  HIP_TRY(hipDeviceSynchronize());
+  if (pause && env->ea_running)  // per-step demand from the current step on
+    if (const int rc = ea_stop(env, nullptr, true)) return rc;
+  env->ea_paused = pause;
+  // the per-step path's step_c staging and chain priority (EA runs without staging, chain above the
+  // generation waves); patched into both device descriptors
+  const int32_t stage = pause ? env->obs_stage_pe : 0;
+  const int32_t prio = pause ? env->chain_prio_pe : 1;
+  const char* os = getenv("MSC_OBS_STAGE");
+  const char* cp = getenv("MSC_CHAIN_PRIO");
+  env->c.obs_stage = (!pause && os && atoi(os) != 0) ? env->obs_stage_pe : stage;
+  env->c.chain_prio = (!pause && cp && atoi(cp) == 0) ? 0 : prio;
+  for (int b = 0; b < 2; b++) {
+    HIP_TRY(hipMemcpy(&env->dev[b].c.obs_stage, &env->c.obs_stage, sizeof(int32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(&env->dev[b].c.chain_prio, &env->c.chain_prio, sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  return 0;
+}
+
 int msc_env_set_chain_priority(msc_env* env, int32_t enabled) {
   if (!env) return set_err(-1, "null env");
   const int32_t v = enabled != 0 ? 1 : 0;
@@ -972,17 +1012,20 @@ int msc_env_read_timing(msc_env* env, double* demand_ms, double* step_ms, int64_
   return 0;
 }
 
-int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* slots, int32_t* active) {
+int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* slots, int32_t* active,
+                           double* env_steps_per_launch) {
   if (!env) return set_err(-1, "null env");
   const int n = env->n_tea < env->t_cap ? env->n_tea : env->t_cap;
-  double sum = 0.0;
+  double sum = 0.0, work = 0.0;
   for (int i = 0; i < n; i++) {
     HIP_TRY(hipEventSynchronize(env->tev_ea[2 * i + 1]));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, env->tev_ea[2 * i], env->tev_ea[2 * i + 1]));
     sum += ms;
+    work += i < (int)env->tea_work.size() ? env->tea_work[i] : 0.0;
   }
   if (ea_ms) *ea_ms = n ? sum / n : 0.0;
+  if (env_steps_per_launch) *env_steps_per_launch = n ? work / n : 0.0;
   if (n_ea) *n_ea = n;
   if (slots) *slots = env->c.ea_S;
   if (active) *active = env->ea_running && env->ea_cur >= 0 ? 1 : 0;

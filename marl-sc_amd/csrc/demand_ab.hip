@@ -30,6 +30,23 @@
 
 namespace msc {
 
+#ifdef MSC_PROF
+// in-kernel cycle accounting (profiling build: make prof, tools/prof_demand.py): [0] A cycles, [1] A
+// at barriers, [2] A rounds, [3] A waves, [4] B cycles, [5] B at barriers, [6] B replaying,
+// [7] generator cycles, [8] generators at barriers, [9] generator waves
+__device__ unsigned long long g_prof_ab[16];
+#define ABP_T(v) const unsigned long long v = (unsigned long long)clock64()
+#define ABP_DECL(v) unsigned long long v = 0
+#define ABP_ADD(v, x) (v) += (x)
+#define ABP_FLUSH(i, v) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof_ab[i], (v))
+#else
+#define ABP_T(v)
+#define ABP_DECL(v)
+#define ABP_ADD(v, x)
+#define ABP_FLUSH(i, v)
+#endif
+
 #ifndef MSC_BOOK_PRIO
 #define MSC_BOOK_PRIO 2  // s_setprio of the bookkeeper wave
 #endif
@@ -199,21 +216,30 @@ __global__ __launch_bounds__(BS * (2 + G)) __attribute__((amdgpu_waves_per_eu(MS
       }
     };
     int tgt = UCAP;
+    ABP_T(g0);
+    ABP_DECL(gbar);
     if (valid) gen_to(UCAP);
     __syncthreads();
     for (int ci = 0;; ci++) {
       const int rdp = rdv[(ci & 1) * BS + lane];
       tgt = unit_quota(tgt, rdp);
       if (valid) gen_to(tgt);
+      ABP_T(gb0);
       __syncthreads();
+      ABP_ADD(gbar, (unsigned long long)clock64() - gb0);
       if (!more[ci & 1]) break;
       const int need = rdv[((ci + 1) & 1) * BS + lane] + UHS * UD;
       if (__ballot(valid && tgt < need) != 0) {
         tgt = tgt > need ? tgt : need;
         if (valid) gen_to(tgt);
+        ABP_T(gb1);
         __syncthreads();
+        ABP_ADD(gbar, (unsigned long long)clock64() - gb1);
       }
     }
+    ABP_FLUSH(7, (unsigned long long)clock64() - g0);
+    ABP_FLUSH(8, gbar);
+    ABP_FLUSH(9, 1ull);
     return;
   }
 
@@ -252,10 +278,17 @@ __global__ __launch_bounds__(BS * (2 + G)) __attribute__((amdgpu_waves_per_eu(MS
       }
     };
     __syncthreads();  // the initial fill
+    ABP_T(b0);
+    ABP_DECL(bbar);
+    ABP_DECL(brep);
     int ptgt = UCAP, rd_start = 0;  // the generators' fill target, restated (their top-up barrier)
     for (int ci = 0;; ci++) {
+      ABP_T(br0);
       if (ci > 0) replay((ci - 1) & 1);
+      ABP_T(bb0);
+      ABP_ADD(brep, bb0 - br0);
       __syncthreads();
+      ABP_ADD(bbar, (unsigned long long)clock64() - bb0);
       if (!more[ci & 1]) {
         replay(ci & 1);
         break;
@@ -265,10 +298,15 @@ __global__ __launch_bounds__(BS * (2 + G)) __attribute__((amdgpu_waves_per_eu(MS
       const int need = rd_a + UHS * UD;
       if (__ballot(valid && ptgt < need) != 0) {
         ptgt = ptgt > need ? ptgt : need;
+        ABP_T(bb1);
         __syncthreads();
+        ABP_ADD(bbar, (unsigned long long)clock64() - bb1);
       }
       rd_start = rd_a;
     }
+    ABP_FLUSH(4, (unsigned long long)clock64() - b0);
+    ABP_FLUSH(5, bbar);
+    ABP_FLUSH(6, brep);
     if (!valid) return;
     if (b.n > cap) atomicOr(s.err, ERR_ORDER_OVERFLOW);
     if constexpr (!EA) s.n_orders[e] = b.n > cap ? cap : b.n;
@@ -299,7 +337,11 @@ __global__ __launch_bounds__(BS * (2 + G)) __attribute__((amdgpu_waves_per_eu(MS
     }
   }
   int ptgt = UCAP, rd_start = 0;  // the generators' fill target and the chunk's start position
+  ABP_T(a0);
+  ABP_DECL(abar);
+  ABP_DECL(arounds);
   for (int ci = 0;; ci++) {
+    ABP_ADD(arounds, UHS);
     uint8_t* lg = ulog + ((ci & 1) * BS + lane) * UHS;
 #pragma unroll 1
     for (int hs = 0; hs < UHS; hs++) {
@@ -331,17 +373,25 @@ __global__ __launch_bounds__(BS * (2 + G)) __attribute__((amdgpu_waves_per_eu(MS
     const bool any = __ballot(a.live) != 0;
     rdv[((ci + 1) & 1) * BS + lane] = a.rd;
     if (lane == 0) more[ci & 1] = any ? 1 : 0;
+    ABP_T(ab0);
     __syncthreads();
+    ABP_ADD(abar, (unsigned long long)clock64() - ab0);
     if (!any) break;
     // the generators' refill decision, restated: their top-up barrier (if any) is joined here
     ptgt = unit_quota(ptgt, rd_start);
     const int need = a.rd + UHS * UD;
     if (__ballot(valid && ptgt < need) != 0) {
       ptgt = ptgt > need ? ptgt : need;
+      ABP_T(ab1);
       __syncthreads();
+      ABP_ADD(abar, (unsigned long long)clock64() - ab1);
     }
     rd_start = a.rd;
   }
+  ABP_FLUSH(0, (unsigned long long)clock64() - a0);
+  ABP_FLUSH(1, abar);
+  ABP_FLUSH(2, arounds);
+  ABP_FLUSH(3, 1ull);
   if (!valid) return;
   if constexpr (!EA) {
     pcg_advance(r0, (uint64_t)a.rd);
@@ -518,6 +568,17 @@ static void launch_ab_k(const EnvConst& c, const DevEnv* d, hipStream_t st, cons
                        dim3(BS * (2 + G)), ab_lds_fixed(), st, d, EaLaunch{0, 0, 0, 0, 0, 0, 0});
   }
 }
+
+#ifdef MSC_PROF
+extern "C" int msc_debug_prof_ab(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof_ab), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof_ab), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 bool demand_ab_supported(const EnvConst& c) { return c.demand_uni != 0 && c.K >= 1 && c.K <= UD && c.K <= 8; }
 

@@ -1849,7 +1849,7 @@ static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t 
     launch_demand_seq(c, d, st, ea);
     return;
   }
-  if (G == 3 && c.demand_impl == 0 && demand_ab_supported(c)) {  // the split parser (demand_ab.hip)
+  if (G == 3 && c.demand_impl == 7 && demand_ab_supported(c)) {  // the split parser (demand_ab.hip, A/B)
     launch_demand_ab(c, d, st, ea);
     return;
   }

@@ -352,6 +352,14 @@ class RolloutCollector:
             self.obs_filter = MeanStdObsFilter(W * L, dev, n_lanes=len(envs))
         elif obs_filter not in ("off", None):
             raise ValueError(f"obs_filter must be 'off' or 'meanstd', not {obs_filter!r}")
+        # Episode-ahead demand beside the policy kernels: at 4,096 envs it lifts the rollout (the
+        # per-step demand chain would bound the step), at 32,768 the background generation takes the
+        # MLP kernels' CU slots (C3 MAPPO rollout 1.15 -> 1.32 ms per step, profiles/r04/ab_ea_c3.txt),
+        # so lanes of >= 16,384 envs step with per-step pipelined demand. MSC_ROLLOUT_EA=0|1 forces it.
+        rea = os.environ.get("MSC_ROLLOUT_EA")
+        for x in envs:
+            if getattr(x, "ea_slots", 0) and hasattr(x, "set_episode_ahead"):
+                x.set_episode_ahead(x.n_envs < 16384 if rea is None else rea != "0")
         self._lanes, off = [], 0
         for x in envs:
             st = torch.cuda.Stream(device=dev) if len(envs) > 1 else None

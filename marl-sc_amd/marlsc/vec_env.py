@@ -173,6 +173,12 @@ class VecInventoryEnv:
         abi.check(abi.lib().msc_env_read_timing(self._h, C.byref(d), C.byref(s), C.byref(nd), C.byref(ns)))
         return {"demand_ms": d.value, "step_ms": s.value, "n_demand": nd.value, "n_step": ns.value}
 
+    def set_episode_ahead(self, enabled: bool) -> None:
+        """msc_env_set_episode_ahead: switch episode-ahead demand off (per-step pipelined demand from the
+        current step on) or back on (from the next common episode start); results are identical."""
+        with torch.cuda.device(self.device):
+            abi.check(abi.lib().msc_env_set_episode_ahead(self._h, 1 if enabled else 0))
+
     def ea_memory(self) -> Dict[str, int]:
         """Episode-ahead memory (msc_env_ea_memory): the create-time budget and the bytes allocated."""
         b, a = C.c_int64(), C.c_int64()
@@ -183,9 +189,11 @@ class VecInventoryEnv:
         """Episode-ahead demand (msc_env_read_timing_ea): mean device ms of the timed episode
         generation launches, their count, slots per env (0: off) and whether the current episode
         reads a generated slot."""
-        ms, n, slots, act = C.c_double(), C.c_int64(), C.c_int32(), C.c_int32()
-        abi.check(abi.lib().msc_env_read_timing_ea(self._h, C.byref(ms), C.byref(n), C.byref(slots), C.byref(act)))
-        return {"ea_ms": ms.value, "n_ea": n.value, "slots": slots.value, "active": bool(act.value)}
+        ms, n, slots, act, work = C.c_double(), C.c_int64(), C.c_int32(), C.c_int32(), C.c_double()
+        abi.check(abi.lib().msc_env_read_timing_ea(self._h, C.byref(ms), C.byref(n), C.byref(slots), C.byref(act),
+                                                   C.byref(work)))
+        return {"ea_ms": ms.value, "n_ea": n.value, "slots": slots.value, "active": bool(act.value),
+                "ea_env_steps_per_launch": work.value}
 
     def alloc_info(self) -> Dict[str, torch.Tensor]:
         """Device buffers for msc_step_info (the reference's collect_step_info dict)."""

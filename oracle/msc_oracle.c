@@ -4,8 +4,9 @@
  * A deliberately plain, scalar C restatement of the reference's environment hot path. Every
  * function follows one reference function and says which (paths relative to /root/reference).
  * numpy 2.2's Generator pieces are restated from their published algorithms (SeedSequence
- * hash-mix pool, PCG64 XSL-RR 128/64, next_double, Poisson multiplication method for lam < 10,
- * 32-bit buffered Lemire bounded integers); pinned by tests/golden/rng_streams.npz.
+ * hash-mix pool, PCG64 XSL-RR 128/64, next_double, Poisson multiplication method for lam < 10 and
+ * PTRS for lam >= 10, 32-bit buffered Lemire bounded integers); pinned by tests/golden/rng_streams.npz
+ * and tests/golden/poisson_ptrs.npz.
  *
  * dtype flow mirrors numpy exactly (f32 buffers where the reference keeps f32, f64 elsewhere),
  * and reductions use numpy's order (sequential for n < 8, 8-way unrolled pairwise blocks up to
@@ -380,10 +381,10 @@ orc_env* orc_create(const msc_env_desc* d, int64_t E, uint32_t base_seed, uint32
     o->enlam_o = (double*)malloc(sizeof(double) * R);
     o->enlam_q = (double*)malloc(sizeof(double) * R * K);
     for (int r = 0; r < R; r++) {
-      if (!(o->lo[r] < 10.0) || !(o->lo[r] >= 0.0)) FAIL("lambda_orders must be in [0, 10)");
+      if (!(o->lo[r] < 1e6) || !(o->lo[r] >= 0.0)) FAIL("lambda_orders must be in [0, 1e6)");
       o->enlam_o[r] = exp(-o->lo[r]);
       for (int s = 0; s < K; s++) {
-        if (!(o->lq[r * K + s] < 10.0)) FAIL("lambda_quantity must be < 10");
+        if (!(o->lq[r * K + s] < 20000.0)) FAIL("lambda_quantity must be < 20000");
         o->enlam_q[r * K + s] = exp(-o->lq[r * K + s]);
       }
     }

@@ -614,3 +614,51 @@ def test_ptrs_rates_env_vs_oracle(monkeypatch, ea, lo, lq):
     cfg = make_synthetic_env_config(4, 16, 3, episode_length=7, lambda_orders=lo, lambda_quantity=lq)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     _lockstep(spec, 96, 17, seed=4, check_every=2)
+
+
+@pytest.mark.parametrize("ea", ["0", "1"])
+def test_split_parser_demand_vs_oracle(monkeypatch, ea):
+    # the split chain / bookkeeper demand parser (MSC_DEMAND_IMPL=ab, csrc/demand_ab.hip; an A/B
+    # variant, measured slower than the default unit parser) against the oracle, per step and episode-ahead
+    monkeypatch.setenv("MSC_DEMAND_IMPL", "ab")
+    monkeypatch.setenv("MSC_EA", ea)
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=9)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 192, 21, seed=6, check_every=4)
+
+
+def test_episode_ahead_runtime_switch_stays_exact(monkeypatch):
+    # msc_env_set_episode_ahead: episode-ahead demand switched off mid-episode (per-step pipelined
+    # demand from that step on) and back on (restarting at the next common episode start) leaves
+    # every observation, reward and state bit-exact with per-step demand; the step_c staging / chain
+    # priority patched on each switch change nothing either
+    monkeypatch.setenv("MSC_ALLOC_IMPL", "lane")
+    for k in ("MSC_EA", "MSC_EA_SLOTS", "MSC_OBS_STAGE", "MSC_OBS_RING_REG"):
+        monkeypatch.delenv(k, raising=False)
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=6)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    E = 160
+    a = _vec(spec, E, base_seed=41, episode_ahead=4)
+    b = _vec(spec, E, base_seed=41, episode_ahead=0)
+    assert a.ea_slots == 4 and b.ea_slots == 0
+    a.reset(), b.reset()
+    rng = np.random.default_rng(9)
+    on = 0
+    for t in range(70):
+        if t == 20:
+            a.set_episode_ahead(False)
+        if t == 33:
+            a.set_episode_ahead(True)
+        act = torch.from_numpy(rng.uniform(-1, 1, (E, 8, 5)).astype(np.float32)).cuda()
+        oa = a.step(act)[0].clone()
+        ob = b.step(act)[0].clone()
+        assert torch.equal(oa, ob), f"step {t}"
+        assert torch.equal(a.rewards, b.rewards), f"step {t}"
+        on += int(a.read_timing_ea()["active"])
+        if t % 5 == 2:
+            sa, sb = a.read_state(), b.read_state()
+            for k in ("rng", "inventory", "timestep", "episode_counter"):
+                assert np.array_equal(sa[k], sb[k]), f"{k} at step {t}"
+    assert on > 20
+    a.check()
+    b.check()
