@@ -132,6 +132,7 @@ def time_env(env, pool, steps: int, warmup: int, world: int, ea: bool = False):
     # the timing pass: 50 steps, or with episode-ahead demand 2.5 episodes (a generation launch covers
     # whole episodes of every env: one or two per episode in steady state)
     kp = min(steps, 50) if not ea else int(2.5 * env.spec.episode_length)
+    kp = int(os.environ.get("MSC_BENCH_TIMING_STEPS", kp))
     env.set_timing(kp)
     for i in range(kp):
         env.step(pool[i % len(pool)])
@@ -201,8 +202,9 @@ def c2_line(args, rank: int):
     rc = RolloutConfig.from_algorithm_config(algo)
     torch.manual_seed(0)
     module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
-    # one refill period (4 episodes = 4 rollouts) timed, so the window holds one generation launch
-    t_roll = time_rollout(env, module, T, 1, seed=rank, warm=4, reps=4) if args.rollout_T > 0 else 0.0
+    # two refill periods (8 episodes = 8 rollouts) timed after one: a one-period window read 0.215 or
+    # 0.29 ms per step depending on where in the refill schedule it fell (profiles/r04/ab_c2_roll.txt)
+    t_roll = time_rollout(env, module, T, 1, seed=rank, warm=4, reps=8) if args.rollout_T > 0 else 0.0
     a_h, c_h = rc.actor["hidden_sizes"], rc.critic["hidden_sizes"]
     out = {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x {spec.K} SKUs "
                        f"(BASELINE configs[1])",

@@ -58,11 +58,27 @@ constexpr int SC_WIN = 64;   // orders ranked per window (one per lane)
 #define MSC_SC_PRIO 3  // s_setprio: the step chain is the critical path next to the demand generator
 #endif
 
+// Lost regions whose shipment / cost shares are deferred: the region epilogue (on the per-order
+// chain) only records the region, its lost-order count, the units each warehouse shipped to it and the
+// unfulfilled units per SKU; the shares and the lost-sales sums run after the order loop, eight regions
+// per pass (lane = region slot x warehouse) and then one multiply-add per region and (SKU, warehouse)
+// lane, in region order (the reference's summation order, lost_sales_handler.py:113-148 / :170-210).
+constexpr int SC_LR = 64;  // deferred regions per flush
+
 // LDS per wave: the window's order records, epilogue scratch
 struct ScWaveLds {
   uint4 rec[SC_WIN];
   int32_t iscr[64];
   double dscr[64];
+};
+// and, when the lost-sales shares are deferred, the deferred lost regions (after the SC_WAVES
+// ScWaveLds blocks; not allocated otherwise)
+struct ScLostLds {
+  int32_t lr_acc[SC_LR * 8];  // [i][w] units warehouse w shipped to deferred region i (GW <= 8)
+  int32_t lr_ug[SC_LR * 8];   // [i][s] unfulfilled units of SKU s (K <= 6)
+  int32_t lr_r[SC_LR];        // region id
+  int32_t lr_cnt[SC_LR];      // lost orders
+  double lr_wt[64];           // one pass's shares [i % (64 / GW)][w]
 };
 constexpr size_t sc_tab_bytes(int R, int GW) { return (size_t)(R | 1) * GW * 16; }
 constexpr size_t SC_TAB_MAX = 32 * 1024;
@@ -96,6 +112,17 @@ __device__ __forceinline__ uint32_t or_groups(uint32_t v) {
   v = a[0] | a[1];
   const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
   return b[0] | b[1];
+}
+// sum of a value over the 64 / GW groups (as or_groups): every lane gets the total of its lane % GW
+template <int GW>
+__device__ __forceinline__ int add_groups(int v) {
+  if constexpr (GW <= 2) v += __builtin_amdgcn_update_dpp(0, v, 0x122, 0xF, 0xF, false);  // row_ror:2
+  if constexpr (GW <= 4) v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);                        // row_ror:8
+  const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+  v = (int)(a[0] + a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+  return (int)(b[0] + b[1]);
 }
 // OR of the 64 / GW groups' GW-bit fields of a ballot
 template <int GW>
@@ -159,6 +186,7 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   double2* Ltab = reinterpret_cast<double2*>(sc_lds);  // [w][R | 1] {of, ov}
   int32_t* Lcl = reinterpret_cast<int32_t*>(sc_lds + (TAB ? sc_tab_bytes(R, GW) : 0));  // [R] closest warehouse
   ScWaveLds* Lw = reinterpret_cast<ScWaveLds*>(Lcl + ((R + 3) & ~3)) + wave;
+  ScLostLds* Ll = reinterpret_cast<ScLostLds*>(reinterpret_cast<ScWaveLds*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) + wave;
   const int RS = R | 1;
   if constexpr (TAB) {
     for (int i = threadIdx.x; i < R * GW; i += blockDim.x) {
@@ -192,6 +220,7 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   const int lost_type = __builtin_amdgcn_readfirstlane(c.lost_type);
   const int maxwh = __builtin_amdgcn_readfirstlane(c.max_wh);
   const bool split = maxwh < W;
+  const bool defer = __builtin_amdgcn_readfirstlane(c.scan_defer) != 0 && !dbg && lost_type != MSC_LOST_CLOSEST;
   const double alpha = sgpr_d(c.alpha);
   const int pps = c.pen_per_sku;
   const double skw_me = sk < K ? c.skw[sk] : 0.0;
@@ -216,6 +245,44 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   const MSC_GLOBAL uint4* src = gp(o.src);
   if (dbg && lane == 0 && info.n_orders) info.n_orders[e] = n;
 
+  // deferred lost regions (see SC_LR): their shares and lost-sales sums, in region order
+  int nl = 0;
+  auto flush_lost = [&]() {
+    constexpr int RPP = 64 / GW;  // regions per share pass
+    for (int i0 = 0; i0 < nl; i0 += RPP) {
+      // shares: lane = (region slot ri, warehouse wl)
+      const int ri = lane / GW, wl = lane % GW, i = i0 + ri;
+      const bool iv = i < nl;
+      const int rr = iv ? Ll->lr_r[i] : 0;
+      double wt = 0.0;
+      if (lost_type == MSC_LOST_COST) {  // softmax(-(of * lost_orders + ov * lost_weight) / alpha)
+        double lw = 0.0;                 // unfulfilled[r] . sku_weights, SKU order
+#pragma unroll
+        for (int j = 0; j < K; j++) lw += (double)(iv ? Ll->lr_ug[i * 8 + j] : 0) * skw[j];
+        const double2 t = tab_at(rr, wl);
+        const double lg = wl < W ? -(t.x * (double)(iv ? Ll->lr_cnt[i] : 0) + t.y * lw) / alpha : -INFINITY;
+        const double mx = sc_group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
+        const double ex = wl < W ? exp(lg - mx) : 0.0;
+        wt = wl < W ? ex / sc_group_np_sum<GW>(ex, W) : 0.0;
+      } else {  // shipment shares; nothing shipped: the closest warehouse
+        const int acc = iv ? Ll->lr_acc[i * 8 + wl] : 0;
+        const int tot = sc_group_reduce<GW>(acc, [](int a, int b) { return a + b; });
+        wt = tot > 0 ? (acc > 0 ? (double)acc / (double)tot : 0.0) : (wl == Lcl[rr] ? 1.0 : 0.0);
+      }
+      Ll->lr_wt[lane] = wt;
+      wave_sync();
+      // lost[w][s] += share(w, r) * unfulfilled(r, s), region by region
+      const int np = nl - i0 < RPP ? nl - i0 : RPP;
+      for (int k = 0; k < np; k++) {
+        const double wk = Ll->lr_wt[k * GW + w];
+        const int ug = Ll->lr_ug[(i0 + k) * 8 + (sk < 8 ? sk : 7)];
+        if (wk != 0.0) lost += wk * (double)ug;
+      }
+      wave_sync();  // lr_wt is rewritten by the next pass
+    }
+    nl = 0;
+  };
+
   // region epilogue: lost sales, outbound cost, home features of region r (uniform)
   auto epilogue = [&](int r) {
     ofix += (double)cnt * of_me;
@@ -225,7 +292,21 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       shh_h = qsr;
       home_done = true;
     }
-    if (lost_cnt > 0 || dbg) {
+    if (lost_cnt > 0 && defer) {
+      // shares deferred (flush_lost): record the region, its lost orders, the units each warehouse
+      // shipped to it (summed over the SKU groups by DPP / permlane swaps) and the unfulfilled units
+      const int acc = add_groups<GW>(qsr);
+      if (sk == 0) Ll->lr_acc[nl * 8 + w] = acc;
+      if (lastp && sk < K) Ll->lr_ug[nl * 8 + sk] = u;  // (the SKU's unfulfilled demand: its last rank lane)
+      if (lane == 0) {
+        Ll->lr_r[nl] = r;
+        Ll->lr_cnt[nl] = lost_cnt;
+      }
+      if (++nl == SC_LR) {
+        wave_sync();
+        flush_lost();
+      }
+    } else if (lost_cnt > 0 || dbg) {
       const int ug = __shfl(u, sk * GW + GW - 1);  // the SKU's unfulfilled demand (kept by its last rank lane)
       if (lost_cnt > 0) {
         double wt = 0.0;
@@ -435,6 +516,10 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   }
   SPROF_T(t_e1);
   if (cur >= 0) epilogue(cur);
+  if (nl > 0) {
+    wave_sync();
+    flush_lost();
+  }
   SPROF_ADD(p_epi, SPROF_NOW() - t_e1);
   SPROF_ADD(p_tot, SPROF_NOW() - t_begin);
   SPROF_FLUSH(0, p_tot);
@@ -481,7 +566,7 @@ static bool alloc_scan_tab(const EnvConst& c, int GW) { return sc_tab_bytes(c.R,
 size_t alloc_scan_lds_bytes(const EnvConst& c) {
   const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : 8;
   return (alloc_scan_tab(c, GW) ? sc_tab_bytes(c.R, GW) : 0) + sizeof(int32_t) * ((c.R + 3) & ~3) +
-         SC_WAVES * sizeof(ScWaveLds);
+         SC_WAVES * sizeof(ScWaveLds) + (c.scan_defer ? SC_WAVES * sizeof(ScLostLds) : 0);
 }
 bool alloc_scan_supported(int W, int K) { return W <= 8 && K <= 6; }
 

@@ -455,6 +455,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     if (c.alloc_impl == 1 && alloc_scan_supported(W, K)) c.alloc_impl = 2;
     if (const char* al = getenv("MSC_ALLOC_IMPL"))
       if (strcmp(al, "scan") == 0) c.alloc_impl = alloc_scan_supported(W, K) ? 2 : 1;
+    c.scan_defer = 1;
+    if (const char* sd = getenv("MSC_SCAN_DEFER")) c.scan_defer = atoi(sd) != 0 ? 1 : 0;
     // episode-ahead Poisson demand when the envs are too few to fill the chip with per-step demand
     // chains (MSC_EA=0|1 forces it off / on)
     c.ea_S = 0;

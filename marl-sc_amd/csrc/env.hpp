@@ -45,6 +45,7 @@ struct EnvConst {
   int32_t alloc_sort;   // step_b_kernel visits envs in descending order of this step's order count (perm)
   int32_t sort_shift;   // order count >> sort_shift = bucket (< SORT_BUCKETS)
   int32_t ea_S;         // episode-ahead demand: episode slots per env (0: off)
+  int32_t scan_defer;   // alloc_scan_kernel: lost-sales shares deferred to a post-pass (MSC_SCAN_DEFER=0: inline)
   int32_t demand_ptrs;  // 1: some Poisson rate >= 10 (numpy's PTRS branch): the sequential sampler demand_seq_kernel
   uint32_t flags;
   int64_t E;

@@ -259,6 +259,7 @@ def normalize_advantages(adv: torch.Tensor, stats: torch.Tensor) -> torch.Tensor
 
 
 NOISE_CHUNK = 16  # rollout steps whose Gaussian noise is drawn in one launch
+_TORCH_NOISE = os.environ.get("MSC_NOISE", "keyed") == "torch"
 
 
 def keyed_normal(shape, row0: int, seed: int, step0: int) -> torch.Tensor:
@@ -397,8 +398,13 @@ class RolloutCollector:
         # per step), keyed by global env id
         if t % NOISE_CHUNK == 0:
             n = min(NOISE_CHUNK, self.T - t)
-            ln.noise = keyed_normal((n,) + tuple(self.actions[t, sl].shape), ln.env.env_index_offset,
-                                    self._noise_seed, self.noise_step + t)
+            if _TORCH_NOISE:  # A/B only: torch's generator (not shard-invariant)
+                if not hasattr(self, "_gen"):
+                    self._gen = torch.Generator(device=obs.device).manual_seed(self._noise_seed & 0x7FFFFFFF)
+                ln.noise = torch.randn((n,) + tuple(self.actions[t, sl].shape), device=obs.device, generator=self._gen)
+            else:
+                ln.noise = keyed_normal((n,) + tuple(self.actions[t, sl].shape), ln.env.env_index_offset,
+                                        self._noise_seed, self.noise_step + t)
         eps = ln.noise[t % NOISE_CHUNK]
         a = None
         if self._ls is not None and hasattr(m, "actor_sample"):

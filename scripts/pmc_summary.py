@@ -17,6 +17,7 @@ import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
 
@@ -47,16 +48,26 @@ for path in glob.glob(f"gpurun_out/pmc_*_{tag}/**/*counter_collection.csv", recu
         if "msc::" not in name or not workload_grid(name, grid):
             continue
         acc[(name, grid)][row["Counter_Name"]].append(float(row["Counter_Value"]))
-# one (instantiation, grid) per base name: the largest grid (a warning if several qualify)
+# one (instantiation, grid) per base name: the one with the most dispatches (the workload's steady
+# state: e.g. the episode-ahead refill launches rather than the one bulk launch that fills the slots
+# at the start), the larger grid on ties
+def n_disp(key):
+    return max(len(x) for x in acc[key].values())
+
+
 chosen = {}
 for (name, grid) in acc:
     b = base_name(name)
     if b in chosen and chosen[b] != (name, grid):
-        print(f"# warning: {b}: several workload-sized groups {chosen[b]} / {(name, grid)}; keeping the larger grid",
-              file=sys.stderr)
-        if grid <= chosen[b][1]:
+        old = chosen[b]
+        print(f"# note: {b}: several workload-sized groups {old} ({n_disp(old)} dispatches) / {(name, grid)} "
+              f"({n_disp((name, grid))}); keeping the one with more dispatches", file=sys.stderr)
+        if (n_disp((name, grid)), grid) <= (n_disp(old), old[1]):
             continue
     chosen[b] = (name, grid)
+only = [x for x in os.environ.get("PMC_ONLY", "").split(",") if x]
+if only:
+    chosen = {b: v for b, v in chosen.items() if b in only}
 traffic, counters, clocks = {}, {}, {}
 dur = {}
 try:
@@ -70,6 +81,7 @@ except FileNotFoundError:
 for b, (name, grid) in sorted(chosen.items()):
     v = {c: sum(x) / len(x) for c, x in acc[(name, grid)].items()}
     v["grid_size"] = grid
+    v["dispatches"] = n_disp((name, grid))
     print(f"{name}")
     for c in sorted(v):
         print(f"   {c:24s} {v[c]:.6g}")
@@ -77,7 +89,7 @@ for b, (name, grid) in sorted(chosen.items()):
         traffic[b] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
         print(f"   => HBM traffic per launch {traffic[b] / 1e6:.2f} MB (2 x FETCH + WRITE)")
     counters[b] = {c: v[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES",
-                                     "SQ_LDS_BANK_CONFLICT", "grid_size") if c in v}
+                                     "SQ_LDS_BANK_CONFLICT", "grid_size", "dispatches") if c in v}
     # effective shader clock: GRBM_GUI_ACTIVE counts busy cycles summed over the 8 XCDs
     # (MI355X_MICROARCH.md), divided by the kernel's mean duration at the same grid (kernel trace)
     d = dur.get((name, grid), 0.0)

@@ -662,3 +662,17 @@ def test_episode_ahead_runtime_switch_stays_exact(monkeypatch):
     assert on > 20
     a.check()
     b.check()
+
+
+@pytest.mark.parametrize("lost", ["shipment", "cost", "closest"])
+@pytest.mark.parametrize("shape", [(8, 64, 5), (3, 7, 2)])
+def test_scan_allocator_lost_sales_handlers_vs_oracle(monkeypatch, lost, shape):
+    # the scan allocator's deferred lost-sales shares (shipment / cost softmax, flushed after the order
+    # loop in region order; csrc/alloc_scan.hip flush_lost) and the inline closest handler, without
+    # step info (the deferred path), against the oracle: rewards 1e-6, observations / state bit-exact;
+    # low inventories so most regions lose orders, more lost regions than one flush holds at 8 x 64
+    monkeypatch.setenv("MSC_ALLOC_IMPL", "scan")
+    W, R, K = shape
+    cfg = make_synthetic_env_config(W, R, K, episode_length=11, lost_sales=lost, initial_inventory=8)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 130, 24, seed=17, check_every=3)
