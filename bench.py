@@ -202,9 +202,11 @@ def c2_line(args, rank: int):
     rc = RolloutConfig.from_algorithm_config(algo)
     torch.manual_seed(0)
     module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
-    # two refill periods (8 episodes = 8 rollouts) timed after one: a one-period window read 0.215 or
-    # 0.29 ms per step depending on where in the refill schedule it fell (profiles/r04/ab_c2_roll.txt)
-    t_roll = time_rollout(env, module, T, 1, seed=rank, warm=4, reps=8) if args.rollout_T > 0 else 0.0
+    # four refill periods (16 episodes = 16 rollouts) timed after one: rollouts run 0.21 ms per step
+    # while no generation launch is in flight and ~0.34 while one is (the launches of one refill take
+    # most of the next 4 rollouts), so a window of one or two periods read 0.21-0.29 ms per step
+    # depending on its phase (profiles/r04/c2_rollout_phases.txt); 16 rollouts average the phases
+    t_roll = time_rollout(env, module, T, 1, seed=rank, warm=4, reps=16) if args.rollout_T > 0 else 0.0
     a_h, c_h = rc.actor["hidden_sizes"], rc.critic["hidden_sizes"]
     out = {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x {spec.K} SKUs "
                        f"(BASELINE configs[1])",
