@@ -1,6 +1,5 @@
 #!/bin/bash
-# Round 4 evidence, part 1: GPU tests, smoke, the default bench line, the C3 profile (kernel trace +
-# PMC passes, scripts/gpu_profile.sh). Stops at the first failure.
+# Round 4 evidence, part 1: GPU tests, smoke, the default bench line. Stops at the first failure.
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -10,6 +9,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; echo "smoke rc=$rc"; tail -n 2 gpurun_out/smoke_r04.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python bench.py > gpurun_out/bench_r04.json.log 2>&1
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
-TAG=r04c3 WORKLOAD=8x64x5x32768 timeout -k 10 900 bash scripts/gpu_profile.sh > gpurun_out/profile_r04c3.log 2>&1
-rc=$?; echo "profile c3 rc=$rc"; tail -n 3 gpurun_out/profile_r04c3.log
-exit $rc
+exit 0
