@@ -46,8 +46,8 @@ typedef struct msc_env msc_env;
 typedef struct ihipStream_t* msc_stream_t; /* == hipStream_t */
 
 #define MSC_ABI_VERSION 2
-#define MSC_MAX_W 16   /* warehouses (agents) per env */
-#define MSC_MAX_K 8    /* SKUs */
+#define MSC_MAX_W 32   /* warehouses (agents) per env (step kernels loop warehouses over <= 16 waves above 16) */
+#define MSC_MAX_K 16   /* SKUs (above 8: the sequential demand sampler and the group allocator) */
 #define MSC_MAX_R 4096 /* demand regions */
 #define MSC_HISTORY 5  /* rolling window, multi_env.py:147 */
 

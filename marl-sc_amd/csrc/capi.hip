@@ -435,6 +435,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       if (strcmp(al, "group") == 0) c.alloc_impl = 1;
       else if (strcmp(al, "lane") == 0) c.alloc_impl = 0;
     }
+    if (W > 16 || K > 8) c.alloc_impl = 1;  // the lane allocator's instantiations stop at 16 x 8
     c.alloc_lpe = 0;
     if (const char* lp = getenv("MSC_ALLOC_LPE")) c.alloc_lpe = atoi(lp);
     // group kernel over empirical demand: a wave runs as many order iterations as its busiest env,

@@ -524,6 +524,14 @@ hipError_t launch_demand_seq(const EnvConst& c, const DevEnv* d, hipStream_t st,
     case 6: launch_seq_k<6>(c, d, st, ea); break;
     case 7: launch_seq_k<7>(c, d, st, ea); break;
     case 8: launch_seq_k<8>(c, d, st, ea); break;
+    case 9: launch_seq_k<9>(c, d, st, ea); break;
+    case 10: launch_seq_k<10>(c, d, st, ea); break;
+    case 11: launch_seq_k<11>(c, d, st, ea); break;
+    case 12: launch_seq_k<12>(c, d, st, ea); break;
+    case 13: launch_seq_k<13>(c, d, st, ea); break;
+    case 14: launch_seq_k<14>(c, d, st, ea); break;
+    case 15: launch_seq_k<15>(c, d, st, ea); break;
+    case 16: launch_seq_k<16>(c, d, st, ea); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

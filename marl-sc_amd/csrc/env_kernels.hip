@@ -21,8 +21,8 @@
 
 namespace msc {
 
-#ifdef MSC_PROF
-// in-kernel cycle accounting (profiling builds only: make prof -> libmarlsc_prof.so)
+#if defined(MSC_PROF) && !defined(MSC_EK_WIDE)
+// in-kernel cycle accounting (profiling builds only: make prof -> libmarlsc_prof.so; SKU counts <= 8)
 __device__ unsigned long long g_prof[16];
 #define PROF_DECL(v) unsigned long long v = 0
 #define PROF_NOW() ((unsigned long long)clock64())
@@ -69,7 +69,8 @@ __device__ __forceinline__ void store_rec(uint4* p, int64_t stride, int region, 
 }
 
 
-// numpy add.reduce order for n <= 8 float32 (sequential below 8, 8-way pairwise at 8)
+// numpy add.reduce order for n <= 128 float32 (pairwise_sum: sequential below 8, else eight
+// strided accumulators over the whole 8-blocks, their fixed tree, then the tail sequentially)
 template <int K>
 __device__ __forceinline__ float np_sum_f32(const float (&a)[K]) {
   if constexpr (K < 8) {
@@ -78,7 +79,17 @@ __device__ __forceinline__ float np_sum_f32(const float (&a)[K]) {
     for (int i = 0; i < K; i++) s += a[i];
     return s;
   } else {
-    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] = a[j];
+#pragma unroll
+    for (int i = 8; i + 8 <= K; i += 8)
+#pragma unroll
+      for (int j = 0; j < 8; j++) r[j] += a[i + j];
+    float s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int i = K - K % 8; i < K; i++) s += a[i];
+    return s;
   }
 }
 
@@ -967,6 +978,7 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
 // The demand stream of env e as of `t_done` steps into the episode held by EA slot `slot`
 // (read_state / save_state / leaving EA mode): the 'demand_sampler' child of the episode's root
 // (s.root, written by the reset that started it) advanced by the draws of those steps.
+#ifndef MSC_EK_WIDE  // (defined once: env_kernels.hip proper)
 __global__ void ea_materialize_kernel(const DevEnv* __restrict__ dp, int32_t slot, int32_t t_done) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
@@ -977,11 +989,12 @@ __global__ void ea_materialize_kernel(const DevEnv* __restrict__ dp, int32_t slo
   pcg_advance(r, s.ea_pos[((int64_t)slot * c.T + (t_done - 1)) * c.E + e]);
   store_rng(s, 0, e, c.E, r);
 }
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Production step: InventoryEnvironment.step (multi_env.py:253-366) as three launches.
 //
-//   step_a_kernel  (block = 64 envs x W waves; wave = warehouse, lane = env): per-env RNG work
+//   step_a_kernel  (block = 64 envs x min(W, 16) waves; wave = warehouse, lane = env): per-env RNG work
 //                  (stochastic lead deviations, empirical window), then orders / lead times /
 //                  pending ring / arrivals / inbound cost for the lane's (w, s) pairs;
 //   step_b_kernel  (group of GW >= W lanes = one env, lane = warehouse): the greedy allocation.
@@ -1000,13 +1013,27 @@ __global__ void ea_materialize_kernel(const DevEnv* __restrict__ dp, int32_t slo
 #define MSC_SA_RING_REG 4  // step_a: pending rings of up to this many slots are read into registers
 #endif
 constexpr int SA_RING_REG = MSC_SA_RING_REG;
+// waves of a step_a / step_c block: one per warehouse up to 16 warehouses (LOOP = false: the
+// kernel has no warehouse loop); above 16 warehouses (or above 8 SKUs, whose K-wide register
+// arrays need the larger per-lane budget of a WB = 4-wave block) each wave takes warehouses
+// w, w + WB, ... (LOOP = true)
+constexpr int STEP_WAVES = 16;
+template <int WB, bool LOOP, typename F>
+__device__ __forceinline__ void each_warehouse(int wave, int W, F&& f) {
+  if constexpr (LOOP) {
+    for (int w = wave; w < W; w += WB) f(w);
+  } else {
+    if (wave < W) f(wave);
+  }
+}
+// waves per block of the LOOP instantiations: 4 above 8 SKUs, else 16
+__host__ __device__ constexpr int step_loop_waves(int K) { return K > 8 ? 4 : STEP_WAVES; }
 // REG: the register-ring instantiation (the fixed-lead path holds the K rings in registers: ~2x the
 // VGPRs, which costs co-residency beside the demand kernel at 32,768 envs; used with obs_ring_reg)
-template <int K, bool DBG, bool REG = false>
-__global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+template <int K, bool DBG, bool REG = false, int WB = STEP_WAVES, bool LOOP = false>
+__global__ __launch_bounds__(BS * WB) void step_a_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
-  extern __shared__ __attribute__((aligned(16))) int32_t Ldev[];  // stochastic: [w*K+s][lane] deviations
   __shared__ int32_t Lt[BS];
   const int W = c.W, WK = W * K, RING = c.RING;
   const int64_t E = c.E;
@@ -1021,13 +1048,19 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __
     const int t = s.t[e];
     Lt[lane] = t;
     if (stoch) {  // lead_time_sampler.sample(): all W*K deviations every step (multi_env.py:866)
+      // each actual lead time max(1, elt + deviation) goes straight to the ring slot of this step's
+      // order (the arrival pass of the warehouse waves skips that slot)
+      const int slot = t % RING;
+      auto put = [&](int i, int64_t dev) {
+        const int l = c.elt[i] + (int)dev;
+        s.ring_l[((int64_t)i * RING + slot) * E + e] = (uint8_t)(l > 1 ? l : 1);
+      };
       Pcg64 rl = load_rng(s, 1, e, E);
       if (c.dev_per_sku) {  // SKU-major column_stack order (lead_time_sampler.py:181-185)
         for (int sk = 0; sk < K; sk++)
-          for (int w = 0; w < W; w++)
-            Ldev[(w * K + sk) * BS + lane] = (int32_t)bounded_int(rl, -c.maxdev[sk], (int64_t)c.maxdev[sk] + 1);
+          for (int w = 0; w < W; w++) put(w * K + sk, bounded_int(rl, -c.maxdev[sk], (int64_t)c.maxdev[sk] + 1));
       } else {
-        for (int i = 0; i < WK; i++) Ldev[i * BS + lane] = (int32_t)bounded_int(rl, -c.maxdev[0], (int64_t)c.maxdev[0] + 1);
+        for (int i = 0; i < WK; i++) put(i, bounded_int(rl, -c.maxdev[0], (int64_t)c.maxdev[0] + 1));
       }
       store_rng(s, 1, e, E, rl);
     }
@@ -1038,89 +1071,136 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __
     }
   }
   __syncthreads();
-  if (wave >= W || !ev) return;
-  const int w = wave, t = Lt[lane];
+  if (!ev) return;
+  const int t = Lt[lane];
   const int slot = t % RING;
-  double inbF = 0.0, inbV = 0.0;
-  if constexpr (REG && K <= 5) {
-  if (RING <= SA_RING_REG && !stoch) {
-    // (fixed lead times; <= 5 SKUs, whose rings fit the register budget) Every load of the K SKUs first, then the arithmetic, then the stores: vector loads and stores
-    // retire through one counter (vmcnt), so a load issued after a store waits for it (the loop
-    // below stores the new order before it reads the ring for arrivals, K times)
-    float a[K];
-    int inc_old[K], inv[K], rv[K][SA_RING_REG];
+  // one warehouse per wave (LOOP: each wave takes w, w + WB, ...)
+  auto warehouse = [&](const int w) {
+    double inbF = 0.0, inbV = 0.0;
+    if constexpr (REG && K <= 5) {
+    if (RING <= SA_RING_REG && !stoch) {
+      // (fixed lead times; <= 5 SKUs, whose rings fit the register budget) Every load of the K SKUs first, then the arithmetic, then the stores: vector loads and stores
+      // retire through one counter (vmcnt), so a load issued after a store waits for it (the loop
+      // below stores the new order before it reads the ring for arrivals, K times)
+      float a[K];
+      int inc_old[K], inv[K], rv[K][SA_RING_REG];
 #pragma unroll
-    for (int sk = 0; sk < K; sk++) {
-      const int i = w * K + sk;
-      a[sk] = io.actions[(e * W + w) * K + sk];
-      inc_old[sk] = s.inc[i * E + e];
-      inv[sk] = s.inv[i * E + e];
-      const int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
+      for (int sk = 0; sk < K; sk++) {
+        const int i = w * K + sk;
+        a[sk] = io.actions[(e * W + w) * K + sk];
+        inc_old[sk] = s.inc[i * E + e];
+        inv[sk] = s.inv[i * E + e];
+        const int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
 #pragma unroll
-      for (int q = 0; q < SA_RING_REG; q++) rv[sk][q] = q < RING ? rq[q * E] : 0;
+        for (int q = 0; q < SA_RING_REG; q++) rv[sk][q] = q < RING ? rq[q * E] : 0;
+      }
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {
+        const int i = w * K + sk;
+        int pend = 0;
+#pragma unroll
+        for (int q = 0; q < SA_RING_REG; q++) pend += rv[sk][q];
+        const double prm = c.act_param[sk];  // _rescale_actions_to_quantities (multi_env.py:795-848)
+        double q;
+        if (c.action_type == MSC_ACTION_DIRECT) {
+          q = rint((double)((a[sk] + 1.0f) / 2.0f) * prm);
+          q = q < 0.0 ? 0.0 : (q > prm ? prm : q);
+        } else if (c.action_type == MSC_ACTION_DEMAND_CENTERED) {
+          q = rint(prm * (double)a[sk]) + (double)inc_old[sk];
+          q = q < 0.0 ? 0.0 : q;
+        } else {
+          const double target = (double)((a[sk] + 1.0f) / 2.0f) * prm;
+          q = rint((target - (double)(float)inc_old[sk]) - (double)(float)pend);
+          q = q < 0.0 ? 0.0 : q;
+        }
+        const int qi = (int)q;
+        const int elt = c.elt[i];
+        int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
+        if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = inv[sk];
+        // _apply_arrivals: orders whose actual lead time equals their age arrive (actual arrival == t)
+        int iv = inv[sk];
+#pragma unroll
+        for (int jr = 0; jr < SA_RING_REG; jr++) {
+          int age = (t - jr) % RING;
+          if (age < 0) age += RING;
+          const bool arrive = jr < RING && jr != slot && rv[sk][jr] != 0 && elt == age;
+          iv += arrive ? rv[sk][jr] : 0;
+          if (arrive) rq[jr * E] = 0;
+        }
+        rq[slot * E] = qi;  // _apply_orders: the slot of order time t
+        s.inv[i * E + e] = iv;
+        s.inc[i * E + e] = 0;
+        if (qi > 0) inbF += c.inF[i];
+        inbV += ((double)qi * c.skw[sk]) * c.inV[i];
+        if (dbg) {
+          if (info.pending_total) info.pending_total[e * WK + i] = pend;
+          if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
+        }
+      }
+      s.sc_inb[w * E + e] = inbF + inbV;
+      return;
+    }
+    }
+    if (RING <= SA_RING_REG && !stoch) {
+      // (the low-register form: one SKU at a time, each SKU's loads issued together before its stores)
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {
+        const int i = w * K + sk;
+        int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
+        const float a = io.actions[(e * W + w) * K + sk];
+        const int inc_old = s.inc[i * E + e];
+        int iv = s.inv[i * E + e];
+        int rv[SA_RING_REG];
+#pragma unroll
+        for (int q = 0; q < SA_RING_REG; q++) rv[q] = q < RING ? rq[q * E] : 0;
+        int pend = 0;
+#pragma unroll
+        for (int q = 0; q < SA_RING_REG; q++) pend += rv[q];
+        const double prm = c.act_param[sk];  // _rescale_actions_to_quantities (multi_env.py:795-848)
+        double q;
+        if (c.action_type == MSC_ACTION_DIRECT) {
+          q = rint((double)((a + 1.0f) / 2.0f) * prm);
+          q = q < 0.0 ? 0.0 : (q > prm ? prm : q);
+        } else if (c.action_type == MSC_ACTION_DEMAND_CENTERED) {
+          q = rint(prm * (double)a) + (double)inc_old;
+          q = q < 0.0 ? 0.0 : q;
+        } else {
+          const double target = (double)((a + 1.0f) / 2.0f) * prm;
+          q = rint((target - (double)(float)inc_old) - (double)(float)pend);
+          q = q < 0.0 ? 0.0 : q;
+        }
+        const int qi = (int)q;
+        const int elt = c.elt[i];
+        if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = iv;
+#pragma unroll
+        for (int jr = 0; jr < SA_RING_REG; jr++) {  // _apply_arrivals (actual arrival == t)
+          int age = (t - jr) % RING;
+          if (age < 0) age += RING;
+          const bool arrive = jr < RING && jr != slot && rv[jr] != 0 && elt == age;
+          iv += arrive ? rv[jr] : 0;
+          if (arrive) rq[jr * E] = 0;
+        }
+        rq[slot * E] = qi;  // _apply_orders: the slot of order time t
+        s.inv[i * E + e] = iv;
+        s.inc[i * E + e] = 0;
+        if (qi > 0) inbF += c.inF[i];
+        inbV += ((double)qi * c.skw[sk]) * c.inV[i];
+        if (dbg) {
+          if (info.pending_total) info.pending_total[e * WK + i] = pend;
+          if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
+        }
+      }
+      s.sc_inb[w * E + e] = inbF + inbV;
+      return;
     }
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       const int i = w * K + sk;
-      int pend = 0;
-#pragma unroll
-      for (int q = 0; q < SA_RING_REG; q++) pend += rv[sk][q];
-      const double prm = c.act_param[sk];  // _rescale_actions_to_quantities (multi_env.py:795-848)
-      double q;
-      if (c.action_type == MSC_ACTION_DIRECT) {
-        q = rint((double)((a[sk] + 1.0f) / 2.0f) * prm);
-        q = q < 0.0 ? 0.0 : (q > prm ? prm : q);
-      } else if (c.action_type == MSC_ACTION_DEMAND_CENTERED) {
-        q = rint(prm * (double)a[sk]) + (double)inc_old[sk];
-        q = q < 0.0 ? 0.0 : q;
-      } else {
-        const double target = (double)((a[sk] + 1.0f) / 2.0f) * prm;
-        q = rint((target - (double)(float)inc_old[sk]) - (double)(float)pend);
-        q = q < 0.0 ? 0.0 : q;
-      }
-      const int qi = (int)q;
-      const int elt = c.elt[i];
-      int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
-      if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = inv[sk];
-      // _apply_arrivals: orders whose actual lead time equals their age arrive (actual arrival == t)
-      int iv = inv[sk];
-#pragma unroll
-      for (int jr = 0; jr < SA_RING_REG; jr++) {
-        int age = (t - jr) % RING;
-        if (age < 0) age += RING;
-        const bool arrive = jr < RING && jr != slot && rv[sk][jr] != 0 && elt == age;
-        iv += arrive ? rv[sk][jr] : 0;
-        if (arrive) rq[jr * E] = 0;
-      }
-      rq[slot * E] = qi;  // _apply_orders: the slot of order time t
-      s.inv[i * E + e] = iv;
-      s.inc[i * E + e] = 0;
-      if (qi > 0) inbF += c.inF[i];
-      inbV += ((double)qi * c.skw[sk]) * c.inV[i];
-      if (dbg) {
-        if (info.pending_total) info.pending_total[e * WK + i] = pend;
-        if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
-      }
-    }
-    s.sc_inb[w * E + e] = inbF + inbV;
-    return;
-  }
-  }
-  if (RING <= SA_RING_REG && !stoch) {
-    // (the low-register form: one SKU at a time, each SKU's loads issued together before its stores)
-#pragma unroll
-    for (int sk = 0; sk < K; sk++) {
-      const int i = w * K + sk;
-      int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
       const float a = io.actions[(e * W + w) * K + sk];
       const int inc_old = s.inc[i * E + e];
-      int iv = s.inv[i * E + e];
-      int rv[SA_RING_REG];
-#pragma unroll
-      for (int q = 0; q < SA_RING_REG; q++) rv[q] = q < RING ? rq[q * E] : 0;
+      int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
       int pend = 0;
-#pragma unroll
-      for (int q = 0; q < SA_RING_REG; q++) pend += rv[q];
+      for (int jr = 0; jr < RING; jr++) pend += rq[jr * E];
       const double prm = c.act_param[sk];  // _rescale_actions_to_quantities (multi_env.py:795-848)
       double q;
       if (c.action_type == MSC_ACTION_DIRECT) {
@@ -1136,17 +1216,22 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __
       }
       const int qi = (int)q;
       const int elt = c.elt[i];
-      if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = iv;
-#pragma unroll
-      for (int jr = 0; jr < SA_RING_REG; jr++) {  // _apply_arrivals (actual arrival == t)
+      rq[slot * E] = qi;  // _apply_orders: the slot of order time t (its actual lead time: wave 0)
+      int inv = s.inv[i * E + e];  // _apply_arrivals: actual arrival == t
+      if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = inv;
+      for (int jr = 0; jr < RING; jr++) {
+        if (jr == slot) continue;
+        const int qq = rq[jr * E];
+        if (qq == 0) continue;
         int age = (t - jr) % RING;
         if (age < 0) age += RING;
-        const bool arrive = jr < RING && jr != slot && rv[jr] != 0 && elt == age;
-        iv += arrive ? rv[jr] : 0;
-        if (arrive) rq[jr * E] = 0;
+        const int l = stoch ? (int)s.ring_l[((int64_t)i * RING + jr) * E + e] : elt;
+        if (l == age) {
+          inv += qq;
+          rq[jr * E] = 0;
+        }
       }
-      rq[slot * E] = qi;  // _apply_orders: the slot of order time t
-      s.inv[i * E + e] = iv;
+      s.inv[i * E + e] = inv;
       s.inc[i * E + e] = 0;
       if (qi > 0) inbF += c.inF[i];
       inbV += ((double)qi * c.skw[sk]) * c.inV[i];
@@ -1156,62 +1241,8 @@ __global__ __launch_bounds__(BS * MSC_MAX_W) void step_a_kernel(const DevEnv* __
       }
     }
     s.sc_inb[w * E + e] = inbF + inbV;
-    return;
-  }
-#pragma unroll
-  for (int sk = 0; sk < K; sk++) {
-    const int i = w * K + sk;
-    const float a = io.actions[(e * W + w) * K + sk];
-    const int inc_old = s.inc[i * E + e];
-    int32_t* rq = s.ring_q + (int64_t)i * RING * E + e;
-    int pend = 0;
-    for (int jr = 0; jr < RING; jr++) pend += rq[jr * E];
-    const double prm = c.act_param[sk];  // _rescale_actions_to_quantities (multi_env.py:795-848)
-    double q;
-    if (c.action_type == MSC_ACTION_DIRECT) {
-      q = rint((double)((a + 1.0f) / 2.0f) * prm);
-      q = q < 0.0 ? 0.0 : (q > prm ? prm : q);
-    } else if (c.action_type == MSC_ACTION_DEMAND_CENTERED) {
-      q = rint(prm * (double)a) + (double)inc_old;
-      q = q < 0.0 ? 0.0 : q;
-    } else {
-      const double target = (double)((a + 1.0f) / 2.0f) * prm;
-      q = rint((target - (double)(float)inc_old) - (double)(float)pend);
-      q = q < 0.0 ? 0.0 : q;
-    }
-    const int qi = (int)q;
-    const int elt = c.elt[i];
-    int lact = elt;
-    if (stoch) {
-      lact = elt + Ldev[i * BS + lane];
-      lact = lact > 1 ? lact : 1;
-    }
-    rq[slot * E] = qi;  // _apply_orders: the slot of order time t
-    if (stoch) s.ring_l[((int64_t)i * RING + slot) * E + e] = (uint8_t)lact;
-    int inv = s.inv[i * E + e];  // _apply_arrivals: actual arrival == t
-    if (dbg && info.inventory_before) info.inventory_before[e * WK + i] = inv;
-    for (int jr = 0; jr < RING; jr++) {
-      if (jr == slot) continue;
-      const int qq = rq[jr * E];
-      if (qq == 0) continue;
-      int age = (t - jr) % RING;
-      if (age < 0) age += RING;
-      const int l = stoch ? (int)s.ring_l[((int64_t)i * RING + jr) * E + e] : elt;
-      if (l == age) {
-        inv += qq;
-        rq[jr * E] = 0;
-      }
-    }
-    s.inv[i * E + e] = inv;
-    s.inc[i * E + e] = 0;
-    if (qi > 0) inbF += c.inF[i];
-    inbV += ((double)qi * c.skw[sk]) * c.inV[i];
-    if (dbg) {
-      if (info.pending_total) info.pending_total[e * WK + i] = pend;
-      if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
-    }
-  }
-  s.sc_inb[w * E + e] = inbF + inbV;
+  };
+  each_warehouse<WB, LOOP>(wave, W, warehouse);
 }
 
 // ---- phase B ------------------------------------------------------------------------------
@@ -1222,6 +1253,7 @@ __device__ __forceinline__ T group_reduce(T v, F op) {
   if constexpr (GW >= 4) v = op(v, dpp_x<1>(v));
   if constexpr (GW >= 8) v = op(v, dpp_x<2>(v));
   if constexpr (GW >= 16) v = op(v, dpp_x<3>(v));
+  if constexpr (GW >= 32) v = op(v, dpp_x<4>(v));
   return v;
 }
 
@@ -1243,10 +1275,11 @@ __host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab) {
   return (size_t)4 * 2 * SB_REC * 16 + (tab ? step_b_tab_bytes(R, W) : 0);
 }
 
-// numpy add.reduce order (np_sum_f64_16) of the group's lane values v_0..v_{n-1} without
-// materialising them: sequential below 8 (lane shuffles), else the 8-accumulator tree as 3 DPP
-// butterfly steps over lanes 0..7 (IEEE addition is commutative, so the butterfly's pairs are
-// numpy's pairs) plus the sequential tail; the result reaches every lane of the group
+// numpy add.reduce order (pairwise_sum, n <= 128) of the group's lane values v_0..v_{n-1} without
+// materialising them: sequential below 8 (lane shuffles), else the eight strided accumulators
+// r_j = v_j + v_{j+8} + ... over the whole 8-blocks (lane j < 8 gathers its column), their tree as
+// 3 DPP butterfly steps over lanes 0..7 (IEEE addition is commutative, so the butterfly's pairs are
+// numpy's pairs), then the tail sequentially; the result reaches every lane of the group
 template <int GW>
 __device__ __forceinline__ double group_np_sum(double v, int n) {
   if (n < 8) {
@@ -1261,16 +1294,21 @@ __device__ __forceinline__ double group_np_sum(double v, int n) {
   if constexpr (GW < 8) {
     return 0.0;  // unreachable: n <= W <= GW
   } else {
-    const double hi = __shfl(v, (threadIdx.x + 8) % GW, GW);  // v_{k+8} for lane k < 8
-    double a = n >= 16 ? v + hi : v;
+    const int m = n - n % 8;  // end of the whole 8-blocks
+    double a = v;
+#pragma unroll
+    for (int b = 8; b < GW; b += 8) {
+      const double x = __shfl(v, (threadIdx.x + b) % GW, GW);  // v_{k+b} for lane k < 8
+      a = b < m ? a + x : a;
+    }
     a = a + dpp_x<0>(a);
     a = a + dpp_x<1>(a);
     a = a + dpp_x<2>(a);
     double r = __shfl(a, 0, GW);
 #pragma unroll
-    for (int i = 8; i < 16; i++) {
-      const double x = __shfl(v, i % GW, GW);
-      r = (n < 16 && i < n) ? r + x : r;
+    for (int i = 8; i < GW; i++) {
+      const double x = __shfl(v, i, GW);
+      r = (i >= m && i < n) ? r + x : r;
     }
     return r;
   }
@@ -1300,6 +1338,7 @@ __device__ __forceinline__ int step_order_count(const EnvConst& c, const EnvStat
 // SORT_BUCKETS buckets of count >> sort_shift; the order within a bucket is arbitrary, as is any
 // permutation: every env's allocation is independent of where it runs). One block; ~10 us at
 // 8,192 envs. Busiest envs first also starts the longest waves first.
+#ifndef MSC_EK_WIDE  // (defined once: env_kernels.hip proper)
 __global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
@@ -1333,9 +1372,11 @@ __global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restri
   __syncthreads();
   for (int64_t e = tid; e < E; e += blockDim.x) s.perm[atomicAdd(&hist[key(e)], 1)] = (int32_t)e;
 }
+#endif
 
+// (above 8 SKUs the K-wide register arrays of a lane need the larger budget of 2 waves per SIMD)
 template <int K, int GW, bool DBG, bool TAB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int W = c.W, WK = W * K, R = c.R;
@@ -1586,6 +1627,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
         if constexpr (GW >= 4) step(dpp64([](int v) { return dpp_x<1>(v); }, mk));
         if constexpr (GW >= 8) step(dpp64([](int v) { return dpp_x<2>(v); }, mk));
         if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
+        if constexpr (GW >= 32) step(dpp64([](int v) { return dpp_x<4>(v); }, mk));
       }
       if (mk == ~0ull) break;  // nobody holds a still-needed SKU
       // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
@@ -1673,11 +1715,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MSC_SB_WPE)
 }
 
 // ---- phase C ------------------------------------------------------------------------------
-// WB: the most warehouses (waves) a block has; blocks of <= 8 waves get up to 256 VGPRs per lane,
-// so the observation builder holds the pending ring in registers without spilling
-template <int K, bool DBG, int WB = MSC_MAX_W>
+// WB: the most waves a block has; blocks of <= 8 waves get up to 256 VGPRs per lane, so the
+// observation builder holds the pending ring in registers without spilling. One warehouse per wave
+// up to STEP_WAVES warehouses (LOOP: each wave takes w, w + WB, ...; see each_warehouse)
+template <int K, bool DBG, int WB = STEP_WAVES, bool LOOP = false>
 __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restrict__ dp, StepIO io) {
-  constexpr int RREG = WB <= 8 ? OBS_RING_REG : 0;
+  constexpr int RREG = (WB <= 8 && K <= 8) ? OBS_RING_REG : 0;
   constexpr bool HSTAT = true;
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
@@ -1688,45 +1731,44 @@ __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restric
   if (MSC_SC_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SC_PRIO);
   if (c.chain_prio) __builtin_amdgcn_s_setprio(3);  // the step chain is the caller's critical path
   const int64_t e = (int64_t)blockIdx.x * BS + lane;
-  const bool act = wave < W && e < E;
-  const int w = wave;
+  const bool ev = e < E;
   const msc_step_info info = io.info;
   constexpr bool dbg = DBG;
-  int t = 0;
-  double rw = 0.0;
-  if (act) {
-    t = s.t[e];
+  const int t = ev ? s.t[e] : 0;
+  if (ev) {
     const int hslot = t % MSC_HISTORY;
-    double hold = 0.0;
-    // the loads first, then the stores (a load issued after a store waits for it: one vmcnt)
-    int iv[K], v[K];
-    float fo[K];
+    each_warehouse<WB, LOOP>(wave, W, [&](const int w) {
+      double hold = 0.0;
+      // the loads first, then the stores (a load issued after a store waits for it: one vmcnt)
+      int iv[K], v[K];
+      float fo[K];
 #pragma unroll
-    for (int sk = 0; sk < K; sk++) {
-      const int i = w * K + sk;
-      iv[sk] = s.inv[i * E + e];
-      v[sk] = s.inc[i * E + e];
-      fo[sk] = s.fc[i * E + e];
-    }
-    const double pen = s.sc_pen[w * E + e], out = s.sc_out[w * E + e], inb = s.sc_inb[w * E + e];
+      for (int sk = 0; sk < K; sk++) {
+        const int i = w * K + sk;
+        iv[sk] = s.inv[i * E + e];
+        v[sk] = s.inc[i * E + e];
+        fo[sk] = s.fc[i * E + e];
+      }
+      const double pen = s.sc_pen[w * E + e], out = s.sc_out[w * E + e], inb = s.sc_inb[w * E + e];
 #pragma unroll
-    for (int sk = 0; sk < K; sk++) {
-      const int i = w * K + sk;
-      s.hist[((int64_t)hslot * WK + i) * E + e] = v[sk];
-      s.fc[i * E + e] = 0.3f * (float)v[sk] + 0.7f * fo[sk];  // EMA forecast (f32)
-      hold += c.hold_per_sku ? (double)iv[sk] * c.hold[sk] : ((double)iv[sk] * c.skw[sk]) * c.hold_scalar;
-    }
-    rw = -((((hold + pen) + out) + inb) * c.scale);
-    Lrw[w * BS + lane] = rw;
-    if (dbg && info.costs) {
-      info.costs[(e * 4 + 0) * W + w] = hold;
-      info.costs[(e * 4 + 1) * W + w] = pen;
-      info.costs[(e * 4 + 2) * W + w] = out;
-      info.costs[(e * 4 + 3) * W + w] = inb;
-    }
+      for (int sk = 0; sk < K; sk++) {
+        const int i = w * K + sk;
+        s.hist[((int64_t)hslot * WK + i) * E + e] = v[sk];
+        s.fc[i * E + e] = 0.3f * (float)v[sk] + 0.7f * fo[sk];  // EMA forecast (f32)
+        hold += c.hold_per_sku ? (double)iv[sk] * c.hold[sk] : ((double)iv[sk] * c.skw[sk]) * c.hold_scalar;
+      }
+      const double rw = -((((hold + pen) + out) + inb) * c.scale);
+      Lrw[w * BS + lane] = rw;
+      if (dbg && info.costs) {
+        info.costs[(e * 4 + 0) * W + w] = hold;
+        info.costs[(e * 4 + 1) * W + w] = pen;
+        info.costs[(e * 4 + 2) * W + w] = out;
+        info.costs[(e * 4 + 3) * W + w] = inb;
+      }
+    });
   }
   __syncthreads();
-  bool trunc = false;
+  const bool trunc = ev && t + 1 >= c.T;
   const int64_t obs_off = e * W * c.L;
   // observation staging: the block's 64 envs x W agents' vectors [env][W*L] (row stride W*L | 1,
   // odd: a wave's 64 lanes write 64 different banks), then written to HBM as the block's one
@@ -1742,17 +1784,17 @@ __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restric
   const int32_t* shh = s.sc_shh + e;
   const int32_t* sht = s.sc_sht + e;
   const int n_hist = t + 1 < MSC_HISTORY ? t + 1 : MSC_HISTORY;
-  if (act) {
-    double v = rw;
-    if (c.scope == MSC_SCOPE_TEAM) {  // team scope: sum over agents in agent order
-      v = 0.0;
-      for (int j = 0; j < W; j++) v += Lrw[j * BS + lane];
-    }
-    io.rew[e * W + w] = (float)v;
-    if (io.rew64) io.rew64[e * W + w] = v;
-    trunc = t + 1 >= c.T;
-    if (trunc && io.final_obs) build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
-    if (!trunc && !c.obs_stage) build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, io.obs + obs_off);
+  if (ev) {
+    double team = 0.0;
+    if (c.scope == MSC_SCOPE_TEAM)  // team scope: sum over agents in agent order
+      for (int j = 0; j < W; j++) team += Lrw[j * BS + lane];
+    each_warehouse<WB, LOOP>(wave, W, [&](const int w) {
+      const double v = c.scope == MSC_SCOPE_TEAM ? team : Lrw[w * BS + lane];
+      io.rew[e * W + w] = (float)v;
+      if (io.rew64) io.rew64[e * W + w] = v;
+      if (trunc && io.final_obs) build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, io.final_obs + obs_off);
+      if (!trunc && !c.obs_stage) build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, io.obs + obs_off);
+    });
   }
   if (c.obs_stage) {
     if (wave == 0) Lskip[lane] = (e >= E || trunc) ? 1 : 0;
@@ -1762,20 +1804,23 @@ __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restric
     for (int p = 0; p < P; p++) {
       const int w0 = p * WP, nw = W - w0 < WP ? W - w0 : WP;
       if (nw <= 0) break;
-      if (act && !trunc && w >= w0 && w < w0 + nw)  // (out + w * L lands at column (w - w0) * L)
-        build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, stg + lane * RS - w0 * L);
+      if (ev && !trunc)
+        each_warehouse<WB, LOOP>(wave, W, [&](const int w) {
+          if (w >= w0 && w < w0 + nw)  // (out + w * L lands at column (w - w0) * L)
+            build_obs_agent<K, RREG, HSTAT>(c, s, e, w, t, n_hist, shh, sht, E, stg + lane * RS - w0 * L);
+        });
       __syncthreads();
       const int NL = nw * L, n = nenv * NL;
       const int dq = nt / NL, dr = nt % NL;  // (env, column) step of the flat index per iteration
-      int ev = (int)threadIdx.x / NL, j = (int)threadIdx.x % NL;
+      int el = (int)threadIdx.x / NL, j = (int)threadIdx.x % NL;
       float* dst = io.obs + e0 * WL + w0 * L;
       for (int i = (int)threadIdx.x; i < n; i += nt) {
-        if (!Lskip[ev]) dst[(int64_t)ev * WL + j] = stg[ev * RS + j];
+        if (!Lskip[el]) dst[(int64_t)el * WL + j] = stg[el * RS + j];
         j += dr;
-        ev += dq;
+        el += dq;
         if (j >= NL) {
           j -= NL;
-          ev += 1;
+          el += 1;
         }
       }
       if (p + 1 < P) __syncthreads();  // the next phase rewrites the stage
@@ -1783,20 +1828,24 @@ __global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restric
   }
   // truncation: reset the env (one sequential RNG pass per env), then every agent's reset obs
   if (__syncthreads_or(trunc ? 1 : 0)) {
-    if (act && w == 0) {
+    if (ev && wave == 0) {
       io.trunc[e] = trunc ? 1 : 0;
       if (trunc) reset_env<K>(c, s, e, 0, nullptr);
       else s.t[e] = t + 1;
     }
     __syncthreads();
-    if (act && trunc) build_obs_agent<K>(c, s, e, w, 0, 0, nullptr, nullptr, 0, io.obs + obs_off);
-  } else if (act && w == 0) {
+    if (trunc)
+      each_warehouse<WB, LOOP>(wave, W, [&](const int w) {
+        build_obs_agent<K>(c, s, e, w, 0, 0, nullptr, nullptr, 0, io.obs + obs_off);
+      });
+  } else if (ev && wave == 0) {
     io.trunc[e] = 0;
     s.t[e] = t + 1;
   }
 }
 
 // flat per-agent obs [E][W][L(1+W)] = local_w || local_0 .. local_{W-1} (multi_env.py:566-573)
+#ifndef MSC_EK_WIDE  // (defined once: env_kernels.hip proper)
 __global__ void obs_flat_kernel(const float* __restrict__ obs, float* __restrict__ flat, int64_t E, int W, int L) {
   const int64_t FL = (int64_t)L * (1 + W);
   const int64_t n = E * W * FL;
@@ -1806,14 +1855,19 @@ __global__ void obs_flat_kernel(const float* __restrict__ obs, float* __restrict
     flat[idx] = j < L ? obs[(e * W + w) * L + j] : obs[e * W * L + (j - L)];
   }
 }
+#endif
 
 // ------------------------------------------------------------------------------------------
-// launchers: dispatch on (K, W bucket)
+// launchers: dispatch on (K, W bucket). The file is compiled three times (translation units that
+// build in parallel): SKU counts 1-8 with every non-template kernel and entry point, and
+// (env_kernels_wide.hip: MSC_EK_WIDE 1 / 2) SKU counts 9-12 / 13-16, whose *_w1 / *_w2 entry
+// points the first part's switches call.
 // ------------------------------------------------------------------------------------------
-int order_record_vec4(int K) { return (1 + K + 7) / 8; }
-
-#define MSC_K_SWITCH(KV, BODY) \
-  switch (KV) {                \
+// (the cases are spelled out: a BODY holding a kernel launch cannot pass through a second macro)
+#ifndef MSC_EK_WIDE
+#define MSC_EK_FN(name) name
+#define MSC_K_SWITCH(KV, BODY, W1, W2) \
+  switch (KV) { \
     case 1: { constexpr int K = 1; BODY; } break; \
     case 2: { constexpr int K = 2; BODY; } break; \
     case 3: { constexpr int K = 3; BODY; } break; \
@@ -1822,35 +1876,80 @@ int order_record_vec4(int K) { return (1 + K + 7) / 8; }
     case 6: { constexpr int K = 6; BODY; } break; \
     case 7: { constexpr int K = 7; BODY; } break; \
     case 8: { constexpr int K = 8; BODY; } break; \
+    default: \
+      if ((KV) > 8 && (KV) <= 12) { W1; } \
+      if ((KV) > 12 && (KV) <= MSC_MAX_K) { W2; } \
+      return hipErrorInvalidValue; \
+  }
+#define MSC_EK_DECL(S)                                                                                    \
+  hipError_t launch_reset_##S(const EnvConst& c, const DevEnv* d, const uint8_t* mask, const uint32_t* new_roots, \
+                              int32_t flags, float* obs, hipStream_t st);                                 \
+  hipError_t launch_demand_##S(const EnvConst& c, const DevEnv* d, hipStream_t st);                       \
+  hipError_t launch_demand_ea_##S(const EnvConst& c, const DevEnv* d, const EaLaunch& ea, hipStream_t st); \
+  hipError_t launch_step_##S(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen, hipStream_t st);
+MSC_EK_DECL(w1)
+MSC_EK_DECL(w2)
+#undef MSC_EK_DECL
+
+int order_record_vec4(int K) { return (1 + K + 7) / 8; }
+
+void launch_alloc_sort(const DevEnv* d, const StepIO& io, hipStream_t st) {
+  hipLaunchKernelGGL(alloc_sort_kernel, dim3(1), dim3(1024), 0, st, d, io);
+}
+#elif MSC_EK_WIDE == 1
+#define MSC_EK_FN(name) name##_w1
+#define MSC_K_SWITCH(KV, BODY, W1, W2) \
+  switch (KV) { \
+    case 9: { constexpr int K = 9; BODY; } break; \
+    case 10: { constexpr int K = 10; BODY; } break; \
+    case 11: { constexpr int K = 11; BODY; } break; \
+    case 12: { constexpr int K = 12; BODY; } break; \
     default: return hipErrorInvalidValue; \
   }
+void launch_alloc_sort(const DevEnv* d, const StepIO& io, hipStream_t st);
+#else
+#define MSC_EK_FN(name) name##_w2
+#define MSC_K_SWITCH(KV, BODY, W1, W2) \
+  switch (KV) { \
+    case 13: { constexpr int K = 13; BODY; } break; \
+    case 14: { constexpr int K = 14; BODY; } break; \
+    case 15: { constexpr int K = 15; BODY; } break; \
+    case 16: { constexpr int K = 16; BODY; } break; \
+    default: return hipErrorInvalidValue; \
+  }
+void launch_alloc_sort(const DevEnv* d, const StepIO& io, hipStream_t st);
+#endif
 
 static dim3 grid_for(int64_t E, int epw = BS) { return dim3((unsigned)((E + epw - 1) / epw)); }
 
-hipError_t launch_reset(const EnvConst& c, const DevEnv* d, const uint8_t* mask, const uint32_t* new_roots,
-                        int32_t flags, float* obs, hipStream_t st) {
-  MSC_K_SWITCH(c.K, hipLaunchKernelGGL(reset_kernel<K>, grid_for(c.E), dim3(BS), 0, st, d, mask, new_roots, flags, obs));
+hipError_t MSC_EK_FN(launch_reset)(const EnvConst& c, const DevEnv* d, const uint8_t* mask, const uint32_t* new_roots,
+                                   int32_t flags, float* obs, hipStream_t st) {
+  MSC_K_SWITCH(c.K, hipLaunchKernelGGL(reset_kernel<K>, grid_for(c.E), dim3(BS), 0, st, d, mask, new_roots, flags, obs),
+               return launch_reset_w1(c, d, mask, new_roots, flags, obs, st),
+               return launch_reset_w2(c, d, mask, new_roots, flags, obs, st));
   return hipGetLastError();
 }
 
 static size_t park_fixed(const EnvConst& c) { return c.demand_impl == 5 ? park4_lds_fixed() : unit_lds_fixed(); }
-static bool park_lds_tables(const EnvConst& c) {
+[[maybe_unused]] static bool park_lds_tables(const EnvConst& c) {
   return park_fixed(c) + (size_t)(2 + c.K) * c.R * sizeof(double) <= 40 * 1024;
 }
+#ifndef MSC_EK_WIDE
 size_t demand_lds_bytes(const EnvConst& c) {
   return park_fixed(c) + (park_lds_tables(c) ? (size_t)(2 + c.K) * c.R * sizeof(double) : 0);
 }
+#endif
 
 template <int K, int G>
 static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea) {
   using DFn = void (*)(const DevEnv*);
   using UFn = void (*)(const DevEnv*, EaLaunch);
   if (c.demand_ptrs) {  // a rate >= 10: numpy's PTRS branch, the sequential sampler (demand_ab.hip)
-    launch_demand_seq(c, d, st, ea);
+    (void)launch_demand_seq(c, d, st, ea);
     return;
   }
   if (G == 3 && c.demand_impl == 7 && demand_ab_supported(c)) {  // the split parser (demand_ab.hip, A/B)
-    launch_demand_ab(c, d, st, ea);
+    (void)launch_demand_ab(c, d, st, ea);
     return;
   }
   const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
@@ -1875,50 +1974,70 @@ static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t 
 
 template <int K>
 static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea = nullptr) {
-  if (c.demand_gen == 1)
+  if constexpr (K > 8) {  // above 8 SKUs: the sequential sampler (demand_ab.hip), per step or episode-ahead
+    (void)launch_demand_seq(c, d, st, ea);
+  } else if (c.demand_gen == 1) {
     launch_split_demand<K, 1>(c, d, st, ea);
-  else if (c.demand_gen == 2)
+  } else if (c.demand_gen == 2) {
     launch_split_demand<K, 2>(c, d, st, ea);
-  else
+  } else {
     launch_split_demand<K, 3>(c, d, st, ea);
+  }
 }
 
-hipError_t launch_demand(const EnvConst& c, const DevEnv* d, hipStream_t st) {
-  MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st));
+hipError_t MSC_EK_FN(launch_demand)(const EnvConst& c, const DevEnv* d, hipStream_t st) {
+  MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st), return launch_demand_w1(c, d, st), return launch_demand_w2(c, d, st));
   return hipGetLastError();
 }
 
-hipError_t launch_demand_ea(const EnvConst& c, const DevEnv* d, const EaLaunch& ea, hipStream_t st) {
+hipError_t MSC_EK_FN(launch_demand_ea)(const EnvConst& c, const DevEnv* d, const EaLaunch& ea, hipStream_t st) {
   if (ea.nslots < 1) return hipSuccess;
-  MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st, &ea));
+  MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st, &ea), return launch_demand_ea_w1(c, d, ea, st),
+               return launch_demand_ea_w2(c, d, ea, st));
   return hipGetLastError();
 }
 
+#ifndef MSC_EK_WIDE
 hipError_t launch_ea_materialize(const EnvConst& c, const DevEnv* d, int slot, int t_done, hipStream_t st) {
   hipLaunchKernelGGL(ea_materialize_kernel, grid_for(c.E, 256), dim3(256), 0, st, d, slot, t_done);
   return hipGetLastError();
 }
+#endif
 
 template <int K>
 static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen, hipStream_t st) {
   if (gen && c.demand_type == MSC_DEMAND_POISSON) launch_demand_k<K>(c, d, st);
   using KFn = void (*)(const DevEnv*, StepIO);
   // three phase kernels, group-per-env allocation
-  const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : c.W <= 8 ? 8 : 16;
+  const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : c.W <= 8 ? 8 : c.W <= 16 ? 16 : 32;
   const bool dbg = io.has_info != 0;  // collect_step_info: the instrumented instantiations
-  KFn a = c.obs_ring_reg ? (dbg ? (KFn)step_a_kernel<K, true, true> : (KFn)step_a_kernel<K, false, true>)
-                         : (dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>);
-  KFn cc = (c.W <= 8 && c.obs_ring_reg) ? (dbg ? (KFn)step_c_kernel<K, true, 8> : (KFn)step_c_kernel<K, false, 8>)
-                    : (dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>);
+  // step_a / step_c: one wave per warehouse, or (> 16 warehouses, > 8 SKUs) LW waves looping
+  constexpr int LW = step_loop_waves(K);
+  int nwv = c.W;
+  KFn a, cc;
+  auto loop_forms = [&] {
+    nwv = c.W < LW ? c.W : LW;
+    a = dbg ? (KFn)step_a_kernel<K, true, false, LW, true> : (KFn)step_a_kernel<K, false, false, LW, true>;
+    cc = dbg ? (KFn)step_c_kernel<K, true, LW, true> : (KFn)step_c_kernel<K, false, LW, true>;
+  };
+  if constexpr (K > 8) {
+    loop_forms();
+  } else if (c.W > STEP_WAVES) {
+    loop_forms();
+  } else {
+    a = c.obs_ring_reg ? (dbg ? (KFn)step_a_kernel<K, true, true> : (KFn)step_a_kernel<K, false, true>)
+                       : (dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>);
+    cc = (c.W <= 8 && c.obs_ring_reg) ? (dbg ? (KFn)step_c_kernel<K, true, 8> : (KFn)step_c_kernel<K, false, 8>)
+                                      : (dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>);
+  }
   const bool tab = step_b_tab_bytes(c.R, c.W) <= STEP_B_TAB_MAX;
   KFn b;
 #define MSC_SB(GWV)                                                                                   \
   (dbg ? (tab ? (KFn)step_b_kernel<K, GWV, true, true> : (KFn)step_b_kernel<K, GWV, true, false>)   \
        : (tab ? (KFn)step_b_kernel<K, GWV, false, true> : (KFn)step_b_kernel<K, GWV, false, false>))
-  b = GW == 2 ? MSC_SB(2) : GW == 4 ? MSC_SB(4) : GW == 8 ? MSC_SB(8) : MSC_SB(16);
+  b = GW == 2 ? MSC_SB(2) : GW == 4 ? MSC_SB(4) : GW == 8 ? MSC_SB(8) : GW == 16 ? MSC_SB(16) : MSC_SB(32);
 #undef MSC_SB
-  const size_t lds_a = c.lead_type == MSC_LEAD_STOCHASTIC ? (size_t)c.W * K * BS * sizeof(int32_t) : 0;
-  hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * c.W), lds_a, st, d, io);
+  hipLaunchKernelGGL(a, grid_for(c.E), dim3(BS * nwv), 0, st, d, io);
   if (c.alloc_impl == 0) {
     const hipError_t ea = launch_alloc_lane(c, d, io, st);
     if (ea != hipSuccess) return ea;
@@ -1926,29 +2045,32 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     const hipError_t ea = launch_alloc_scan(c, d, io, st);
     if (ea != hipSuccess) return ea;
   } else {
-    if (c.alloc_sort) hipLaunchKernelGGL(alloc_sort_kernel, dim3(1), dim3(1024), 0, st, d, io);
+    if (c.alloc_sort) launch_alloc_sort(d, io, st);
     hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
   }
   const int stage_w = c.obs_stage ? (c.W + (c.obs_stage > 1 ? c.obs_stage : 1) - 1) / (c.obs_stage > 1 ? c.obs_stage : 1) : 0;
   const size_t lds_c = (size_t)c.W * BS * sizeof(double) +
                        (c.obs_stage ? (size_t)BS * ((stage_w * c.L) | 1) * sizeof(float) + BS * sizeof(int32_t) : 0);
-  hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * c.W), lds_c, st, d, io);
+  hipLaunchKernelGGL(cc, grid_for(c.E), dim3(BS * nwv), lds_c, st, d, io);
   return hipGetLastError();
 }
 
-hipError_t launch_step(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen, hipStream_t st) {
-  MSC_K_SWITCH(c.K, return launch_step_k<K>(c, d, io, gen, st));
+hipError_t MSC_EK_FN(launch_step)(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen, hipStream_t st) {
+  MSC_K_SWITCH(c.K, return launch_step_k<K>(c, d, io, gen, st), return launch_step_w1(c, d, io, gen, st),
+               return launch_step_w2(c, d, io, gen, st));
   return hipSuccess;
 }
 
+#ifndef MSC_EK_WIDE
 hipError_t launch_obs_flat(const EnvConst& c, const float* obs, float* flat, hipStream_t st) {
   const int64_t n = c.E * c.W * (int64_t)c.L * (1 + c.W);
   const int64_t blocks = (n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536;
   hipLaunchKernelGGL(obs_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, st, obs, flat, c.E, c.W, c.L);
   return hipGetLastError();
 }
+#endif
 
-#ifdef MSC_PROF
+#if defined(MSC_PROF) && !defined(MSC_EK_WIDE)
 extern "C" int msc_debug_prof(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
   if (reset) {

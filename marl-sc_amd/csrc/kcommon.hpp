@@ -60,13 +60,18 @@ __device__ __forceinline__ double np_sum_f64_16(const double (&v)[16], int n) {
 
 // Butterfly partner exchange inside a group of GW lanes with DPP (a VALU operand modifier, no LDS
 // round trip): step 0 pairs lanes i ^ 1 and step 1 lanes i ^ 2 (quad_perm), step 2 the two quads
-// of an 8-lane row half (row_half_mirror), step 3 the two halves of a 16-lane row (row_mirror).
-// Every step pairs lanes whose partial results cover disjoint halves, so min / sum reductions end
-// with the group result in every lane.
+// of an 8-lane row half (row_half_mirror), step 3 the two halves of a 16-lane row (row_mirror),
+// step 4 (32-lane groups, > 16 warehouses) lanes i ^ 16 across rows (DPP stays inside a row: a
+// lane shuffle). Every step pairs lanes whose partial results cover disjoint halves, so min / sum
+// reductions end with the group result in every lane.
 template <int S>
 __device__ __forceinline__ int dpp_x(int v) {
-  constexpr int ctrl = S == 0 ? 0xB1 : S == 1 ? 0x4E : S == 2 ? 0x141 : 0x140;
-  return __builtin_amdgcn_update_dpp(0, v, ctrl, 0xF, 0xF, false);
+  if constexpr (S == 4) {
+    return __shfl_xor(v, 16);
+  } else {
+    constexpr int ctrl = S == 0 ? 0xB1 : S == 1 ? 0x4E : S == 2 ? 0x141 : 0x140;
+    return __builtin_amdgcn_update_dpp(0, v, ctrl, 0xF, 0xF, false);
+  }
 }
 template <int S>
 __device__ __forceinline__ double dpp_x(double v) {

@@ -11,7 +11,7 @@ import os
 from pathlib import Path
 
 ABI_VERSION = 2
-MAX_W, MAX_K, MAX_R, HISTORY = 16, 8, 4096, 5
+MAX_W, MAX_K, MAX_R, HISTORY = 32, 16, 4096, 5
 
 DEMAND = {"poisson": 0, "empirical": 1}
 ACTION = {"direct": 0, "demand_centered": 1, "base_stock": 2}

@@ -391,6 +391,10 @@ def test_launch_timing_counts_and_results_unchanged(monkeypatch):
                                              # limit: long units, many carried products
     (16, 9, 4, 6.0, 0.5, 7.5, "shipment"),   # widest group (16 warehouses per env)
     (12, 7, 3, 4.0, 0.6, 5.0, "closest"),    # masked warehouse slots (12 of 16; 3 of 4 per lane)
+    (24, 11, 12, 3.0, 0.6, 4.0, "cost"),     # past the 16 x 8 shapes: 32-lane groups (24 of 32),
+                                             # warehouse waves looping, the sequential sampler
+    (32, 6, 16, 2.0, 0.5, 3.0, "shipment"),  # the caps: 32 warehouses, 16 SKUs
+    (20, 5, 9, 1.5, 0.7, 2.0, "closest"),
 ])
 @pytest.mark.usefixtures("alloc_impl_lpe")
 def test_demand_and_allocation_edges_vs_oracle(W, R, K, lo, p, lq, lost):
@@ -398,6 +402,23 @@ def test_demand_and_allocation_edges_vs_oracle(W, R, K, lo, p, lq, lost):
                                     lambda_quantity=lq, lost_sales=lost)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     _lockstep(spec, 192, 32, seed=11, check_every=4)
+
+
+@pytest.mark.parametrize("W,K,dev,scope", [(24, 12, [0, 1, 2, 3] * 3, "team"), (17, 10, 2, "agent"),
+                                           (8, 5, [1, 0, 2, 1, 3], "agent")])
+def test_wide_stochastic_leads_all_features_vs_oracle(W, K, dev, scope):
+    # stochastic lead times past 16 warehouses (step_a's warehouse loop; every actual lead time is
+    # written by the per-env RNG wave), all observation features with aggregates (K > 8: numpy's
+    # 8-accumulator f32 sums), ratio normalisation, cost lost sales
+    cfg = make_synthetic_env_config(W, 9, K, episode_length=14, features={k: True for k in FEATURE_CONFIG_YAML},
+                                    lost_sales="cost",
+                                    scope=scope)
+    cfg["components"]["lead_time_sampler"] = {"type": "stochastic", "params": {
+        "expected_lead_times": [[1 + (w + k) % 4 for k in range(K)] for w in range(W)],
+        "deviation": {"type": "uniform", "max_deviation": dev}}}
+    cfg["initial_inventory"] = {"type": "uniform", "params": {"min": 5, "max": 60}}
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True, "obs_normalization": "ratio"})
+    _lockstep(spec, 130, 30, seed=21, check_every=3)
 
 
 @pytest.mark.parametrize("lost", ["shipment", "closest"])
