@@ -138,8 +138,21 @@ def time_env(env, pool, steps: int, warmup: int, world: int, ea: bool = False):
         env.step(pool[i % len(pool)])
     tm = env.read_timing()
     tm.update(env.read_timing_ea())
-    tm["host_ms_per_step"] = t_host / steps * 1e3
     env.set_timing(0)
+    # host enqueue cost per step: bursts of 10 steps enqueued right after a synchronize (inside the
+    # long timed loop the launch queue fills once the device falls behind, and enqueue then waits
+    # for the device: t_host / steps is that back-pressured figure, kept as enqueue_ms_per_step)
+    tb, nb = 0.0, 0
+    for _ in range(20):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(10):
+            env.step(pool[i % len(pool)])
+        tb += time.perf_counter() - t1
+        nb += 10
+    torch.cuda.synchronize()
+    tm["host_ms_per_step"] = tb / nb * 1e3
+    tm["enqueue_ms_per_step"] = t_host / steps * 1e3
     env.check()
     return dt, tm
 
@@ -212,7 +225,7 @@ def c2_line(args, rank: int):
                        f"(BASELINE configs[1])",
            "value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "ms_per_step": round(dt / steps * 1e3, 4),
            "steps": steps, "warmup": warm, "obs_normalization": norm,
-           "host_ms_per_step": round(tm["host_ms_per_step"], 4),
+           "host_ms_per_step": round(tm["host_ms_per_step"], 4), "enqueue_ms_per_step": round(tm["enqueue_ms_per_step"], 4),
            "demand": (f"episode-ahead: future episodes drawn on a side stream ({tm['slots']} slots per env, "
                       f"generated in 50-step chunks, several slots per launch)" if tm["slots"] else "per step (pipelined)"),
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
@@ -278,7 +291,7 @@ def c5_line(args, rank: int):
                        f"empirical demand trace ({mean_orders:.0f} orders per step on average) (BASELINE configs[4])",
            "value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "ms_per_step": round(dt / steps * 1e3, 4),
            "steps": steps, "warmup": args.warmup, "obs_normalization": meta.get("obs_normalization", "off"),
-           "host_ms_per_step": round(tm["host_ms_per_step"], 4),
+           "host_ms_per_step": round(tm["host_ms_per_step"], 4), "enqueue_ms_per_step": round(tm["enqueue_ms_per_step"], 4),
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4)}}
     # the step kernels (no demand kernel: the trace window is read inside step_a) against the VALU
     # issue peak and their HBM bytes, from the PMC passes of this workload (profiles/traffic.json)
@@ -432,6 +445,7 @@ def main():
         ea_line = {"value": round(E * spec.W * 8 * T_ep / dt_ea, 1), "unit": "agent-steps/s",
                    "ms_per_step": round(dt_ea / (8 * T_ep) * 1e3, 4), "steps": 8 * T_ep, "warmup": 6 * T_ep,
                    "slots": tm_ea["slots"], "host_ms_per_step": round(tm_ea["host_ms_per_step"], 4),
+                   "enqueue_ms_per_step": round(tm_ea["enqueue_ms_per_step"], 4),
                    "kernels_ms": {"step_kernels": round(tm_ea["step_ms"], 4),
                                   DEMAND_KERNEL + "_ea": round(tm_ea["ea_ms"], 3),
                                   "ea_env_steps_per_launch": int(tm_ea["ea_env_steps_per_launch"])},
@@ -612,6 +626,8 @@ def main():
             "kernels_ms": {DEMAND_KERNEL: round(t_demand * 1e3, 4), "step_kernels": round(t_step * 1e3, 4),
                            **({DEMAND_KERNEL + "_ea": round(t_ea * 1e3, 3), "ea_env_steps_per_launch": int(ea_work),
                                "ea_slots": tm["slots"]} if ea_regime else {})},
+            "host_ms_per_step": round(tm["host_ms_per_step"], 4),
+            "enqueue_ms_per_step": round(tm["enqueue_ms_per_step"], 4),
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "bytes_per_launch": int(bytes_dom),

@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <type_traits>
+
 #include "env.hpp"
 #include "kcommon.hpp"
 
@@ -65,23 +67,31 @@ constexpr int SC_WIN = 64;   // orders ranked per window (one per lane)
 // lane, in region order (the reference's summation order, lost_sales_handler.py:113-148 / :170-210).
 constexpr int SC_LR = 64;  // deferred regions per flush
 
-// LDS per wave: the window's order records, epilogue scratch
+// LDS per wave: the window's order records, epilogue scratch (64 entries per SKU slot, see NS)
+template <int NS>
 struct ScWaveLds {
-  uint4 rec[SC_WIN];
-  int32_t iscr[64];
-  double dscr[64];
+  uint4 rec[SC_WIN];  // (also the outbound-variable partials at the end: 128 doubles)
+  int32_t iscr[64 * NS];
+  double dscr[64 * NS];
 };
 // and, when the lost-sales shares are deferred, the deferred lost regions (after the SC_WAVES
 // ScWaveLds blocks; not allocated otherwise)
+template <int GW>
 struct ScLostLds {
-  int32_t lr_acc[SC_LR * 8];  // [i][w] units warehouse w shipped to deferred region i (GW <= 8)
-  int32_t lr_ug[SC_LR * 8];   // [i][s] unfulfilled units of SKU s (K <= 6)
-  int32_t lr_r[SC_LR];        // region id
-  int32_t lr_cnt[SC_LR];      // lost orders
-  double lr_wt[64];           // one pass's shares [i % (64 / GW)][w]
+  static constexpr int LA = GW > 8 ? 16 : 8;
+  int32_t lr_acc[SC_LR * LA];  // [i][w] units warehouse w shipped to deferred region i
+  int32_t lr_ug[SC_LR * 8];    // [i][s] unfulfilled units of SKU s (K <= 6)
+  int32_t lr_r[SC_LR];         // region id
+  int32_t lr_cnt[SC_LR];       // lost orders
+  double lr_wt[64];            // one pass's shares [i % (64 / GW)][w]
 };
 constexpr size_t sc_tab_bytes(int R, int GW) { return (size_t)(R | 1) * GW * 16; }
 constexpr size_t SC_TAB_MAX = 32 * 1024;
+// warehouse lanes per SKU group and SKU slots per lane: GW = the warehouse count rounded up to
+// 2 / 4 / 8 / 16; a wave holds 64 / GW SKU groups, so above 4 SKUs at 16 warehouses each lane
+// carries two (SKU, warehouse) slots (SKUs sg and 4 + sg)
+__host__ __device__ constexpr int sc_gw(int W) { return W <= 2 ? 2 : W <= 4 ? 4 : W <= 8 ? 8 : 16; }
+__host__ __device__ constexpr int sc_ns(int K, int GW) { return (K * GW + 63) / 64; }
 
 // inclusive prefix sum over the GW lanes of each group (p = lane % GW), DPP row shifts inside the
 // 16-lane rows with the lanes whose source belongs to the previous group masked
@@ -94,9 +104,15 @@ __device__ __forceinline__ int group_scan(int x, int p) {
     t = __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);  // row_shr:2
     v += p >= 2 ? t : 0;
   }
-  if constexpr (GW >= 8) {
+  if constexpr (GW == 8) {
     // row_shr:4 into banks 1 and 3 only (lanes 4-7, 12-15 of a row: p >= 4); others add 0
     t = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xA, false);
+    v += t;
+  }
+  if constexpr (GW == 16) {  // a group is a whole row: row_shr:4 into banks 1-3, row_shr:8 into 2-3
+    t = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xE, false);
+    v += t;
+    t = __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xC, false);
     v += t;
   }
   return v;
@@ -107,7 +123,7 @@ template <int GW>
 __device__ __forceinline__ uint32_t or_groups(uint32_t v) {
   if constexpr (GW <= 2) v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false);  // row_ror:2
   if constexpr (GW <= 4) v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);                        // row_ror:8
+  if constexpr (GW <= 8) v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
   const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
   v = a[0] | a[1];
   const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
@@ -118,7 +134,7 @@ template <int GW>
 __device__ __forceinline__ int add_groups(int v) {
   if constexpr (GW <= 2) v += __builtin_amdgcn_update_dpp(0, v, 0x122, 0xF, 0xF, false);  // row_ror:2
   if constexpr (GW <= 4) v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
-  v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);                        // row_ror:8
+  if constexpr (GW <= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
   const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
   v = (int)(a[0] + a[1]);
   const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
@@ -136,23 +152,36 @@ __device__ __forceinline__ T sc_group_reduce(T v, F op) {
   v = op(v, dpp_x<0>(v));
   if constexpr (GW >= 4) v = op(v, dpp_x<1>(v));
   if constexpr (GW >= 8) v = op(v, dpp_x<2>(v));
+  if constexpr (GW >= 16) v = op(v, dpp_x<3>(v));
   return v;
-}
-// numpy add.reduce order of the group's lane values v_0..v_{n-1}, n <= GW <= 8 (sequential)
-template <int GW>
-__device__ __forceinline__ double sc_group_np_sum(double v, int n) {
-  double r = 0.0;
-#pragma unroll
-  for (int j = 0; j < GW; j++) {
-    const double x = __shfl(v, j, GW);
-    r = j < n ? r + x : r;
-  }
-  return r;
 }
 
 __device__ __forceinline__ uint32_t rec_field(const uint4& v, int h) {  // h: compile-time after unrolling
   const uint32_t w = h < 2 ? v.x : h < 4 ? v.y : h < 6 ? v.z : v.w;
   return (h & 1) ? (w >> 16) : (w & 0xffffu);
+}
+
+// 4-bit ranks of up to 8 warehouses in 32 bits, of 16 in 64
+template <int GW>
+using ScRho = typename std::conditional<(GW > 8), uint64_t, uint32_t>::type;
+template <typename T>
+__device__ __forceinline__ T sc_shfl_up1(T v) {
+  if constexpr (sizeof(T) == 8) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, 1), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), 1);
+    return ((T)hi << 32) | lo;
+  } else {
+    return (T)__shfl_up((int)v, 1);
+  }
+}
+template <typename T>
+__device__ __forceinline__ T sc_readlane(T v, int l) {
+  if constexpr (sizeof(T) == 8) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((T)hi << 32) | lo;
+  } else {
+    return (T)__builtin_amdgcn_readlane((int)v, l);
+  }
 }
 
 // Orders of one region with the same cost ranking form a batch: greedy fills of consecutive orders
@@ -165,9 +194,15 @@ __device__ __forceinline__ uint32_t rec_field(const uint4& v, int h) {  // h: co
 // order three threshold counts of D_k, the order masks follow per batch (batches of <= 16 orders;
 // contribution and lost masks in one word OR-reduced over the SKU groups). (With max_splits
 // limiting the warehouses per order every order is its own batch, with per-order ballots.)
+// NS = 2 (16 warehouses, 5-6 SKUs): every per-(SKU, warehouse) quantity is a two-slot array; one
+// ranking, one permute address and one contribution mask serve both slots.
 template <int K, int GW, bool TAB>
-__global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv* __restrict__ dp, StepIO io) {
-  static_assert(K * GW <= 64 && K <= 6, "lane = s * GW + w; one uint4 per order record");
+__global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(GW > 8 ? 3 : 1))) void alloc_scan_kernel(
+    const DevEnv* __restrict__ dp, StepIO io) {
+  constexpr int SPW = 64 / GW;        // SKU groups per wave
+  constexpr int NS = sc_ns(K, GW);    // SKU slots per lane
+  static_assert(K <= 6 && NS <= 2 && GW <= 16, "one uint4 per order record; <= 2 slots");
+  using Rho = ScRho<GW>;
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int W = c.W, R = c.R, WK = W * K;
@@ -176,8 +211,14 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   // the env and everything derived from it -- order counts, loop bounds -- as per-lane values)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t e = (int64_t)blockIdx.x * SC_WAVES + wave;
-  const int sk = lane / GW, w = lane % GW;  // this lane's SKU and warehouse (its rank p in rank space)
-  const bool lv = sk < K && w < W;
+  const int sg = lane / GW, w = lane % GW;  // this lane's SKU group and warehouse (its rank p in rank space)
+  int skj[NS];                              // slot j's SKU
+  bool lvj[NS];
+#pragma unroll
+  for (int j = 0; j < NS; j++) {
+    skj[j] = j * SPW + sg;
+    lvj[j] = skj[j] < K && w < W;
+  }
   const msc_step_info info = io.info;
   const bool dbg = io.has_info != 0;
   if (MSC_SC_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SC_PRIO);
@@ -185,8 +226,10 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   extern __shared__ __attribute__((aligned(16))) char sc_lds[];
   double2* Ltab = reinterpret_cast<double2*>(sc_lds);  // [w][R | 1] {of, ov}
   int32_t* Lcl = reinterpret_cast<int32_t*>(sc_lds + (TAB ? sc_tab_bytes(R, GW) : 0));  // [R] closest warehouse
-  ScWaveLds* Lw = reinterpret_cast<ScWaveLds*>(Lcl + ((R + 3) & ~3)) + wave;
-  ScLostLds* Ll = reinterpret_cast<ScLostLds*>(reinterpret_cast<ScWaveLds*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) + wave;
+  ScWaveLds<NS>* Lw = reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + wave;
+  ScLostLds<GW>* Ll =
+      reinterpret_cast<ScLostLds<GW>*>(reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) + wave;
+  constexpr int LA = ScLostLds<GW>::LA;
   const int RS = R | 1;
   if constexpr (TAB) {
     for (int i = threadIdx.x; i < R * GW; i += blockDim.x) {
@@ -223,22 +266,30 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   const bool defer = __builtin_amdgcn_readfirstlane(c.scan_defer) != 0 && !dbg && lost_type != MSC_LOST_CLOSEST;
   const double alpha = sgpr_d(c.alpha);
   const int pps = c.pen_per_sku;
-  const double skw_me = sk < K ? c.skw[sk] : 0.0;
-  const double pen_me = sk < K ? (pps ? c.pen[sk] : c.pen_scalar) : 0.0;
   const int myhome = w < W ? c.home_of[w] : -1;
   const bool lastp = w == GW - 1;  // the lane of the last rank of its SKU (holds the SKU's total)
 
-  const int64_t gi = (int64_t)(w * K + sk) * E + e;  // this lane's [w*K + s][E] state index
-  int inv = lv ? s.inv[gi] : 0;
-  const int inv0 = inv;
-  int qsr = 0, cnt = 0, u = 0, dsum = 0, lost_cnt = 0;
+  // per slot: [w*K + s][E] state index, inventory, shipped-to-region, unfulfilled (last rank lane),
+  // incoming demand of the region; lost sales; outbound-variable accumulator; home features.
   // ofix: sum_r count * fixed; ovacc: sum_r shipped(w, r, s) * variable (the SKU weights applied once
   // at the end: out_var_w = sum_s w_s ovacc_s, reward_calculator.py:141-142 reordered)
-  double lost = 0.0, ofix = 0.0, ovacc = 0.0, of_me = 0.0, ov_me = 0.0;
-  int inc_h = 0, shh_h = 0;
+  int64_t gi[NS];
+  int inv[NS], inv0[NS], qsr[NS], u[NS], dsum[NS], inc_h[NS], shh_h[NS], fi[NS];
+  double lost[NS], ovacc[NS];
+#pragma unroll
+  for (int j = 0; j < NS; j++) {
+    gi[j] = (int64_t)(w * K + skj[j]) * E + e;
+    inv[j] = lvj[j] ? s.inv[gi[j]] : 0;
+    inv0[j] = inv[j];
+    qsr[j] = u[j] = dsum[j] = inc_h[j] = shh_h[j] = 0;
+    lost[j] = ovacc[j] = 0.0;
+    fi[j] = skj[j] < K ? 1 + skj[j] : 7;  // this slot's 16-bit field of a record (field 7 is 0: K <= 6)
+  }
+  int cnt = 0, lost_cnt = 0;
+  double ofix = 0.0, of_me = 0.0, ov_me = 0.0;
   bool home_done = false;
   int cur = -1;
-  uint32_t cur_rho = 0xFFFFFFFFu;
+  Rho cur_rho = ~Rho(0);
 
   const OrderSrc o = order_src<1>(c, s, io, e);
   const int n = __builtin_amdgcn_readfirstlane(o.n);
@@ -263,9 +314,9 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
         const double lg = wl < W ? -(t.x * (double)(iv ? Ll->lr_cnt[i] : 0) + t.y * lw) / alpha : -INFINITY;
         const double mx = sc_group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
         const double ex = wl < W ? exp(lg - mx) : 0.0;
-        wt = wl < W ? ex / sc_group_np_sum<GW>(ex, W) : 0.0;
+        wt = wl < W ? ex / group_np_sum<GW>(ex, W) : 0.0;
       } else {  // shipment shares; nothing shipped: the closest warehouse
-        const int acc = iv ? Ll->lr_acc[i * 8 + wl] : 0;
+        const int acc = iv ? Ll->lr_acc[i * LA + wl] : 0;
         const int tot = sc_group_reduce<GW>(acc, [](int a, int b) { return a + b; });
         wt = tot > 0 ? (acc > 0 ? (double)acc / (double)tot : 0.0) : (wl == Lcl[rr] ? 1.0 : 0.0);
       }
@@ -275,8 +326,11 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       const int np = nl - i0 < RPP ? nl - i0 : RPP;
       for (int k = 0; k < np; k++) {
         const double wk = Ll->lr_wt[k * GW + w];
-        const int ug = Ll->lr_ug[(i0 + k) * 8 + (sk < 8 ? sk : 7)];
-        if (wk != 0.0) lost += wk * (double)ug;
+#pragma unroll
+        for (int j = 0; j < NS; j++) {
+          const int ug = Ll->lr_ug[(i0 + k) * 8 + (skj[j] < 8 ? skj[j] : 7)];
+          if (wk != 0.0) lost[j] += wk * (double)ug;
+        }
       }
       wave_sync();  // lr_wt is rewritten by the next pass
     }
@@ -286,18 +340,27 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
   // region epilogue: lost sales, outbound cost, home features of region r (uniform)
   auto epilogue = [&](int r) {
     ofix += (double)cnt * of_me;
-    ovacc += (double)qsr * ov_me;
+#pragma unroll
+    for (int j = 0; j < NS; j++) ovacc[j] += (double)qsr[j] * ov_me;
     if (r == myhome) {
-      inc_h = dsum;
-      shh_h = qsr;
+#pragma unroll
+      for (int j = 0; j < NS; j++) {
+        inc_h[j] = dsum[j];
+        shh_h[j] = qsr[j];
+      }
       home_done = true;
     }
     if (lost_cnt > 0 && defer) {
       // shares deferred (flush_lost): record the region, its lost orders, the units each warehouse
       // shipped to it (summed over the SKU groups by DPP / permlane swaps) and the unfulfilled units
-      const int acc = add_groups<GW>(qsr);
-      if (sk == 0) Ll->lr_acc[nl * 8 + w] = acc;
-      if (lastp && sk < K) Ll->lr_ug[nl * 8 + sk] = u;  // (the SKU's unfulfilled demand: its last rank lane)
+      int qs = 0;
+#pragma unroll
+      for (int j = 0; j < NS; j++) qs += qsr[j];
+      const int acc = add_groups<GW>(qs);
+      if (sg == 0) Ll->lr_acc[nl * LA + w] = acc;
+#pragma unroll
+      for (int j = 0; j < NS; j++)  // (the SKU's unfulfilled demand: its last rank lane)
+        if (lastp && skj[j] < K) Ll->lr_ug[nl * 8 + skj[j]] = u[j];
       if (lane == 0) {
         Ll->lr_r[nl] = r;
         Ll->lr_cnt[nl] = lost_cnt;
@@ -307,14 +370,19 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
         flush_lost();
       }
     } else if (lost_cnt > 0 || dbg) {
-      const int ug = __shfl(u, sk * GW + GW - 1);  // the SKU's unfulfilled demand (kept by its last rank lane)
+      int ug[NS];  // the SKU's unfulfilled demand (kept by its last rank lane)
+#pragma unroll
+      for (int j = 0; j < NS; j++) ug[j] = __shfl(u[j], sg * GW + GW - 1);
       if (lost_cnt > 0) {
         double wt = 0.0;
         if (lost_type == MSC_LOST_CLOSEST) {
           wt = w == Lcl[r] ? 1.0 : 0.0;
         } else {
-          Lw->iscr[lane] = qsr;
-          if (lastp) Lw->dscr[sk] = (double)ug;
+#pragma unroll
+          for (int j = 0; j < NS; j++) {  // [s * GW + w]: slot j's lanes at 64 j + lane
+            Lw->iscr[j * 64 + lane] = qsr[j];
+            if (lastp) Lw->dscr[skj[j]] = (double)ug[j];
+          }
           wave_sync();
           int acc = 0;  // units this warehouse shipped to the region (shipment_quantities[w, r])
 #pragma unroll
@@ -326,46 +394,53 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
             const double lg = w < W ? -(of_me * (double)lost_cnt + ov_me * lw) / alpha : -INFINITY;
             const double mx = sc_group_reduce<GW>(lg, [](double a, double b) { return b > a ? b : a; });
             const double ex = w < W ? exp(lg - mx) : 0.0;
-            wt = w < W ? ex / sc_group_np_sum<GW>(ex, W) : 0.0;
+            wt = w < W ? ex / group_np_sum<GW>(ex, W) : 0.0;
           } else {  // shipment shares; nothing shipped: the closest warehouse
             const int tot = sc_group_reduce<GW>(acc, [](int a, int b) { return a + b; });
             wt = tot > 0 ? (acc > 0 ? (double)acc / (double)tot : 0.0) : (w == Lcl[r] ? 1.0 : 0.0);
           }
-          if (dbg && sk == 0 && w < W) {
+          if (dbg && sg == 0 && w < W) {
             if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] = acc;
           }
           wave_sync();  // iscr / dscr are rewritten by the next epilogue
         }
-        if (wt != 0.0) lost += wt * (double)ug;
+        if (wt != 0.0)
+#pragma unroll
+          for (int j = 0; j < NS; j++) lost[j] += wt * (double)ug[j];
       }
       if (dbg) {
-        if (w == 0 && sk < K) {
-          if (info.demand_per_region) info.demand_per_region[(e * R + r) * K + sk] = dsum;
-          if (info.unfulfilled_demands) info.unfulfilled_demands[(e * R + r) * K + sk] = ug;
+#pragma unroll
+        for (int j = 0; j < NS; j++) {
+          if (w == 0 && skj[j] < K) {
+            if (info.demand_per_region) info.demand_per_region[(e * R + r) * K + skj[j]] = dsum[j];
+            if (info.unfulfilled_demands) info.unfulfilled_demands[(e * R + r) * K + skj[j]] = ug[j];
+          }
+          if (lvj[j] && info.shipment_quantities_by_sku)
+            info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + skj[j]] = qsr[j];
         }
         if (lane == 0 && info.lost_order_counts) info.lost_order_counts[e * R + r] = lost_cnt;
-        if (lv) {
-          if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] = qsr;
-          if (sk == 0 && info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] = cnt;
-        }
+        if (lvj[0] && sg == 0 && info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] = cnt;
         if (info.shipment_quantities && !(lost_cnt > 0 && lost_type != MSC_LOST_CLOSEST)) {
-          Lw->iscr[lane] = qsr;
+#pragma unroll
+          for (int j = 0; j < NS; j++) Lw->iscr[j * 64 + lane] = qsr[j];
           wave_sync();
           int acc = 0;
 #pragma unroll
           for (int j = 0; j < K; j++) acc += Lw->iscr[j * GW + w];
-          if (sk == 0 && w < W) info.shipment_quantities[(e * W + w) * R + r] = acc;
+          if (sg == 0 && w < W) info.shipment_quantities[(e * W + w) * R + r] = acc;
           wave_sync();
         }
       }
     }
-    qsr = cnt = u = dsum = 0;
+#pragma unroll
+    for (int j = 0; j < NS; j++) qsr[j] = u[j] = dsum[j] = 0;
+    cnt = 0;
     lost_cnt = 0;
   };
 
   // order ranks (demand_allocator.py:167-173): 4-bit rank of warehouse w at bits 4w (stable order:
   // lower index first on equal cost); padding warehouses w >= W keep rank w
-  auto rank_of = [&](const uint4& rv) -> uint32_t {
+  auto rank_of = [&](const uint4& rv) -> Rho {
     const int rr = (int)(rv.x & 0xffffu);
     double tw = 0.0;  // order.sku_demands.dot(sku_weights)
 #pragma unroll
@@ -376,19 +451,26 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       const double2 t = tab_at(rr, ww);
       cst[ww] = t.x + t.y * tw;
     }
-    uint32_t rho = 0;
+    // rank of a = the warehouses that sort before it; 32-bit counters per warehouse (a 64-bit
+    // packed sum of 120 selected constants at 16 warehouses ran out of registers)
+    int rk[GW];
+#pragma unroll
+    for (int a = 0; a < GW; a++) rk[a] = a < W ? 0 : a;
 #pragma unroll
     for (int a = 0; a < GW; a++)
 #pragma unroll
       for (int b = a + 1; b < GW; b++)
-        if (b < W) rho += cst[b] < cst[a] ? (1u << (4 * a)) : (1u << (4 * b));
+        if (b < W) {
+          const bool lt = cst[b] < cst[a];
+          rk[a] += lt ? 1 : 0;
+          rk[b] += lt ? 0 : 1;
+        }
+    Rho rho = 0;
 #pragma unroll
-    for (int ww = 0; ww < GW; ww++)
-      if (ww >= W) rho |= (uint32_t)ww << (4 * ww);
+    for (int a = 0; a < GW; a++) rho |= (Rho)rk[a] << (4 * a);
     return rho;
   };
 
-  const int fi = sk < K ? 1 + sk : 7;  // this lane's 16-bit field of a record (field 7 is 0: K <= 6)
   SPROF(p_tot);
   SPROF(p_rank);
   SPROF(p_epi);
@@ -409,9 +491,9 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
     SPROF_T(t_r0);
     // this lane's order (o0 + lane): region, ranking; batch / region starts against the previous order
     const int rg = (int)(rv.x & 0xffffu);
-    const uint32_t rho = lane < nw ? rank_of(rv) : 0u;
+    const Rho rho = lane < nw ? rank_of(rv) : Rho(0);
     int rg_prev = __shfl_up(rg, 1);
-    uint32_t rho_prev = (uint32_t)__shfl_up((int)rho, 1);
+    Rho rho_prev = sc_shfl_up1(rho);
     if (lane == 0) {
       rg_prev = cur;
       rho_prev = cur_rho;
@@ -421,11 +503,14 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
     const uint64_t rstart = __ballot(inw && rg != rg_prev);
     const uint64_t bstart = split ? inwm
                                   : (__ballot(inw && (rg != rg_prev || rho != rho_prev)) | (inwm & 0x0001000100010000ull));
-    uint64_t nzl = 0;  // the window's orders asking for this lane's SKU
+    uint64_t nzl[NS];  // the window's orders asking for each slot's SKU
 #pragma unroll
-    for (int j = 0; j < K; j++) {
-      const uint64_t b = __ballot(inw && rec_field(rv, 1 + j) != 0u);
-      nzl = sk == j ? b : nzl;
+    for (int j = 0; j < NS; j++) nzl[j] = 0;
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+      const uint64_t b = __ballot(inw && rec_field(rv, 1 + q) != 0u);
+#pragma unroll
+      for (int j = 0; j < NS; j++) nzl[j] = skj[j] == q ? b : nzl[j];
     }
     Lw->rec[lane] = rv;
     wave_sync();
@@ -435,8 +520,10 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       const uint64_t later = bstart & ~((2ull << i0) - 1ull);  // batch starts after i0
       const int i1 = __builtin_amdgcn_readfirstlane(later ? (int)__builtin_ctzll(later) : nw);
       const int r = __builtin_amdgcn_readlane(rg, i0);
-      const uint32_t rho_b = (uint32_t)__builtin_amdgcn_readlane((int)rho, i0);
-      int dn = Lh[i0 * 8 + fi];
+      const Rho rho_b = sc_readlane(rho, i0);
+      int dn[NS];
+#pragma unroll
+      for (int j = 0; j < NS; j++) dn[j] = Lh[i0 * 8 + fi[j]];
       if ((rstart >> i0) & 1ull) {  // region boundary (orders are region-major)
         SPROF_T(t_e0);
         if (cur >= 0) epilogue(cur);
@@ -449,42 +536,60 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
       }
       cur_rho = rho_b;
       SPROF_ADD(n_bat, 1);
-      const int paddr = (sk * GW + (int)((rho_b >> (4 * w)) & 0xFu)) << 2;
-      const int x = __builtin_amdgcn_ds_permute(paddr, inv);  // rank space: inventory of the rank-w warehouse
-      const int incl = group_scan<GW>(x, w);
-      const int excl = incl - x;
-      int D = 0, a_prev = 0, cnt_r = 0;
+      const int paddr = (sg * GW + (int)((rho_b >> (4 * w)) & 0xFu)) << 2;
+      int x[NS], incl[NS], excl[NS], a_prev[NS];
+#pragma unroll
+      for (int j = 0; j < NS; j++) {
+        x[j] = __builtin_amdgcn_ds_permute(paddr, inv[j]);  // rank space: inventory of the rank-w warehouse
+        incl[j] = group_scan<GW>(x[j], w);
+        excl[j] = incl[j] - x[j];
+        a_prev[j] = 0;
+      }
+      int cnt_r = 0;
       if (!split) {
-        int c1 = 0, c2 = 0, c3 = 0;  // orders with D <= excl, D < incl, D <= incl
+        int D[NS], c1[NS], c2[NS], c3[NS];  // orders with D <= excl, D < incl, D <= incl
+#pragma unroll
+        for (int j = 0; j < NS; j++) D[j] = c1[j] = c2[j] = c3[j] = 0;
         for (int k = i0; k < i1; k++) {
-          const int d = dn;
-          dn = Lh[(k + 1) * 8 + fi];  // (k + 1 == 64: the scratch after the window, unused)
-          D += d;
-          c1 += D <= excl ? 1 : 0;
-          c2 += D < incl ? 1 : 0;
-          c3 += D <= incl ? 1 : 0;
+#pragma unroll
+          for (int j = 0; j < NS; j++) {
+            const int d = dn[j];
+            dn[j] = Lh[(k + 1) * 8 + fi[j]];  // (k + 1 == 64: the scratch after the window, unused)
+            D[j] += d;
+            c1[j] += D[j] <= excl[j] ? 1 : 0;
+            c2[j] += D[j] < incl[j] ? 1 : 0;
+            c3[j] += D[j] <= incl[j] ? 1 : 0;
+          }
         }
         const int L = i1 - i0;  // <= 16
-        const uint32_t nzb = (uint32_t)(nzl >> i0) & ((1u << L) - 1u);
-        const int hi = c2 < L - 1 ? c2 : L - 1;  // fills from orders c1 .. hi (relative to i0)
-        const uint32_t cm = (x > 0 && hi >= c1) ? nzb & ((2u << hi) - 1u) & ~((1u << c1) - 1u) : 0u;
-        const uint32_t lm = lastp ? nzb & ~((1u << c3) - 1u) : 0u;
+        uint32_t cm = 0u, lm = 0u;
+#pragma unroll
+        for (int j = 0; j < NS; j++) {
+          const uint32_t nzb = (uint32_t)(nzl[j] >> i0) & ((1u << L) - 1u);
+          const int hi = c2[j] < L - 1 ? c2[j] : L - 1;  // fills from orders c1 .. hi (relative to i0)
+          cm |= (x[j] > 0 && hi >= c1[j]) ? nzb & ((2u << hi) - 1u) & ~((1u << c1[j]) - 1u) : 0u;
+          lm |= lastp ? nzb & ~((1u << c3[j]) - 1u) : 0u;
+          const int need = D[j] - excl[j];
+          a_prev[j] = need > 0 ? (need < x[j] ? need : x[j]) : 0;
+          dsum[j] += D[j];
+          u[j] += D[j] - incl[j] > 0 ? D[j] - incl[j] : 0;  // the batch's unfulfilled units (last rank lane)
+        }
         const uint32_t both = or_groups<GW>(cm | (lm << 16));
         cnt_r = __builtin_popcount(both & 0xFFFFu);
         lost_cnt += __builtin_popcount((uint32_t)__builtin_amdgcn_readlane((int)both, GW - 1) >> 16);
-        const int need = D - excl;
-        a_prev = need > 0 ? (need < x ? need : x) : 0;
-        dsum += D;
       } else for (int k = i0; k < i1; k++) {
-        const int d = dn;
-        if (k + 1 < i1) dn = Lh[(k + 1) * 8 + fi];
-        D += d;
-        const int need = D - excl;  // demand left after the cheaper ranks
-        const int a = need > 0 ? (need < x ? need : x) : 0;  // min(inv, max(0, D - prefix))
-        int f = a - a_prev;
-        a_prev = a;
+        int d[NS], f[NS];
+        bool anyf = false;
+#pragma unroll
+        for (int j = 0; j < NS; j++) {
+          d[j] = dn[j];
+          if (k + 1 < i1) dn[j] = Lh[(k + 1) * 8 + fi[j]];
+          const int need = d[j] - excl[j];  // demand left after the cheaper ranks (one-order batch)
+          f[j] = need > 0 ? (need < x[j] ? need : x[j]) : 0;  // min(inv, max(0, d - prefix))
+          anyf |= f[j] > 0;
+        }
         {  // max_splits: only the first max_wh contributing ranks ship (a one-order batch)
-          uint32_t m = fold_groups<GW>(__ballot(f > 0));
+          uint32_t m = fold_groups<GW>(__ballot(anyf));
           if (__builtin_popcount(m) > maxwh) {
             uint32_t keep = 0u;
             for (int q = 0; q < maxwh; q++) {
@@ -493,23 +598,30 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
             }
             m = keep;
           }
-          f = ((m >> w) & 1u) ? f : 0;
-          a_prev = f;
           cnt_r += (int)((m >> w) & 1u);
-          const int rem = d - group_scan<GW>(f, w);  // (this SKU's total in its last rank lane)
-          u += rem;
-          lost_cnt += __ballot(lastp && rem > 0) != 0 ? 1 : 0;
+          bool short_any = false;
+#pragma unroll
+          for (int j = 0; j < NS; j++) {
+            f[j] = ((m >> w) & 1u) ? f[j] : 0;
+            a_prev[j] = f[j];
+            const int rem = d[j] - group_scan<GW>(f[j], w);  // (this SKU's total in its last rank lane)
+            u[j] += rem;
+            short_any |= lastp && rem > 0;
+            dsum[j] += d[j];
+          }
+          lost_cnt += __ballot(short_any) != 0 ? 1 : 0;
         }
-        dsum += d;
       }
-      if (!split) u += D - incl > 0 ? D - incl : 0;  // the batch's unfulfilled units (last rank lane)
-      // total fill and contribution count of the rank back to its warehouse's lane, one bpermute:
-      // fill < 2^24 (<= 64 orders of < 2^16 units), count <= 64
-      const int back = __builtin_amdgcn_ds_bpermute(paddr, (cnt_r << 24) | a_prev);
-      const int fw = back & 0xFFFFFF;
-      inv -= fw;
-      qsr += fw;
-      cnt += (int)((uint32_t)back >> 24);
+      // total fill and contribution count of the rank back to its warehouse's lane, one bpermute per
+      // slot: fill < 2^24 (<= 64 orders of < 2^16 units), count <= 64
+#pragma unroll
+      for (int j = 0; j < NS; j++) {
+        const int back = __builtin_amdgcn_ds_bpermute(paddr, (j == 0 ? cnt_r << 24 : 0) | a_prev[j]);
+        const int fw = back & 0xFFFFFF;
+        inv[j] -= fw;
+        qsr[j] += fw;
+        if (j == 0) cnt += (int)((uint32_t)back >> 24);
+      }
       i0 = i1;
     }
     wave_sync();  // the window is rewritten next
@@ -535,49 +647,61 @@ __global__ __launch_bounds__(64 * SC_WAVES) void alloc_scan_kernel(const DevEnv*
 
   // penalty (reward_calculator.py:134-137): (lost_sales * per-SKU cost, or * sku_weights * cost)
   // summed over SKUs in order; outbound variable cost: sum over SKUs of sku_weight * ovacc
-  Lw->dscr[lane] = pps ? lost * pen_me : (lost * skw_me) * pen_me;
   Lw->rec[lane] = make_uint4(0u, 0u, 0u, 0u);
-  double* Lov = reinterpret_cast<double*>(Lw->rec);
-  Lov[lane] = skw_me * ovacc;
-  wave_sync();
-  if (lv) {
-    s.inv[gi] = inv;
-    s.sc_sht[gi] = inv0 - inv;  // shipped this step = the inventory drop
-    s.sc_shh[gi] = home_done ? shh_h : 0;
-    if (home_done) s.inc[gi] = inc_h;  // (step_a zeroed it: a home region without orders leaves 0)
-    if (dbg) {
-      if (info.lost_sales) info.lost_sales[e * WK + w * K + sk] = lost;
-      if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] = inv0 - inv;
-    }
-    if (sk == 0) {
-      double pen = 0.0, ovar = 0.0;
+  double* Lov = reinterpret_cast<double*>(Lw->rec);  // [s * GW + w] (128 doubles)
 #pragma unroll
-      for (int j = 0; j < K; j++) {
-        pen += Lw->dscr[j * GW + w];
-        ovar += Lov[j * GW + w];
-      }
-      s.sc_pen[w * E + e] = pen;
-      s.sc_out[w * E + e] = ofix + ovar;
+  for (int j = 0; j < NS; j++) {
+    const double skw_me = skj[j] < K ? c.skw[skj[j]] : 0.0;
+    const double pen_me = skj[j] < K ? (pps ? c.pen[skj[j]] : c.pen_scalar) : 0.0;
+    Lw->dscr[j * 64 + lane] = pps ? lost[j] * pen_me : (lost[j] * skw_me) * pen_me;
+    Lov[j * 64 + lane] = skw_me * ovacc[j];
+  }
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < NS; j++) {
+    if (!lvj[j]) continue;
+    s.inv[gi[j]] = inv[j];
+    s.sc_sht[gi[j]] = inv0[j] - inv[j];  // shipped this step = the inventory drop
+    s.sc_shh[gi[j]] = home_done ? shh_h[j] : 0;
+    if (home_done) s.inc[gi[j]] = inc_h[j];  // (step_a zeroed it: a home region without orders leaves 0)
+    if (dbg) {
+      if (info.lost_sales) info.lost_sales[e * WK + w * K + skj[j]] = lost[j];
+      if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + skj[j]] = inv0[j] - inv[j];
     }
+  }
+  if (sg == 0 && w < W) {
+    double pen = 0.0, ovar = 0.0;
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      pen += Lw->dscr[j * GW + w];
+      ovar += Lov[j * GW + w];
+    }
+    s.sc_pen[w * E + e] = pen;
+    s.sc_out[w * E + e] = ofix + ovar;
   }
 }
 
 static bool alloc_scan_tab(const EnvConst& c, int GW) { return sc_tab_bytes(c.R, GW) <= SC_TAB_MAX; }
 size_t alloc_scan_lds_bytes(const EnvConst& c) {
-  const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : 8;
+  const int GW = sc_gw(c.W), NS = sc_ns(c.K, GW);
+  const size_t wave_b = NS > 1 ? sizeof(ScWaveLds<2>) : sizeof(ScWaveLds<1>);
+  const size_t lost_b = GW > 8 ? sizeof(ScLostLds<16>) : sizeof(ScLostLds<8>);
   return (alloc_scan_tab(c, GW) ? sc_tab_bytes(c.R, GW) : 0) + sizeof(int32_t) * ((c.R + 3) & ~3) +
-         SC_WAVES * sizeof(ScWaveLds) + (c.scan_defer ? SC_WAVES * sizeof(ScLostLds) : 0);
+         SC_WAVES * wave_b + (c.scan_defer ? SC_WAVES * lost_b : 0);
 }
-bool alloc_scan_supported(int W, int K) { return W <= 8 && K <= 6; }
+// <= 8 warehouses with <= 6 SKUs (one slot per lane), 9-16 warehouses with <= 6 SKUs (two slots
+// above 4 SKUs)
+bool alloc_scan_supported(int W, int K) { return W <= 16 && K <= 6; }
 
 template <int K>
 static hipError_t launch_scan_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   using KFn = void (*)(const DevEnv*, StepIO);
-  const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : 8;
+  const int GW = sc_gw(c.W);
   const bool t = alloc_scan_tab(c, GW);
   KFn f = GW == 2 ? (t ? (KFn)alloc_scan_kernel<K, 2, true> : (KFn)alloc_scan_kernel<K, 2, false>)
         : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true> : (KFn)alloc_scan_kernel<K, 4, false>)
-                  : (t ? (KFn)alloc_scan_kernel<K, 8, true> : (KFn)alloc_scan_kernel<K, 8, false>);
+        : GW == 8 ? (t ? (KFn)alloc_scan_kernel<K, 8, true> : (KFn)alloc_scan_kernel<K, 8, false>)
+                  : (t ? (KFn)alloc_scan_kernel<K, 16, true> : (KFn)alloc_scan_kernel<K, 16, false>);
   const size_t lds = alloc_scan_lds_bytes(c);
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -452,10 +452,13 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     c.sort_shift = 0;
     while ((maxc >> c.sort_shift) >= SORT_BUCKETS) c.sort_shift++;
     // few envs (BASELINE configs[1]: 4,096): the scan allocator (one env per wave, no
-    // data-dependent loop per order) when the shape fits it (<= 8 warehouses, <= 6 SKUs)
-    if (c.alloc_impl == 1 && alloc_scan_supported(W, K)) c.alloc_impl = 2;
-    if (const char* al = getenv("MSC_ALLOC_IMPL"))
-      if (strcmp(al, "scan") == 0) c.alloc_impl = alloc_scan_supported(W, K) ? 2 : 1;
+    // data-dependent loop per order) at <= 8 warehouses and <= 6 SKUs. It also runs 9-16 warehouses
+    // (MSC_ALLOC_IMPL=scan) but loses there: at C5 (16 x 256, 8,192 envs, ~2.5 orders per region, so
+    // about one order per batch) 1.78 against 0.89 ms per step for the group kernel
+    // (profiles/r04/ab_c5_scan.txt). An explicit MSC_ALLOC_IMPL=group keeps the group kernel.
+    const char* al_env = getenv("MSC_ALLOC_IMPL");
+    if (c.alloc_impl == 1 && !al_env && W <= 8 && alloc_scan_supported(W, K)) c.alloc_impl = 2;
+    if (al_env && strcmp(al_env, "scan") == 0) c.alloc_impl = alloc_scan_supported(W, K) ? 2 : 1;
     c.scan_defer = 1;
     if (const char* sd = getenv("MSC_SCAN_DEFER")) c.scan_defer = atoi(sd) != 0 ? 1 : 0;
     // episode-ahead Poisson demand when the envs are too few to fill the chip with per-step demand

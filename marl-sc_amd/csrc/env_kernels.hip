@@ -1275,44 +1275,7 @@ __host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab) {
   return (size_t)4 * 2 * SB_REC * 16 + (tab ? step_b_tab_bytes(R, W) : 0);
 }
 
-// numpy add.reduce order (pairwise_sum, n <= 128) of the group's lane values v_0..v_{n-1} without
-// materialising them: sequential below 8 (lane shuffles), else the eight strided accumulators
-// r_j = v_j + v_{j+8} + ... over the whole 8-blocks (lane j < 8 gathers its column), their tree as
-// 3 DPP butterfly steps over lanes 0..7 (IEEE addition is commutative, so the butterfly's pairs are
-// numpy's pairs), then the tail sequentially; the result reaches every lane of the group
-template <int GW>
-__device__ __forceinline__ double group_np_sum(double v, int n) {
-  if (n < 8) {
-    double r = 0.0;
-#pragma unroll
-    for (int j = 0; j < (GW < 8 ? GW : 8); j++) {
-      const double x = __shfl(v, j, GW);
-      r = j < n ? r + x : r;
-    }
-    return r;
-  }
-  if constexpr (GW < 8) {
-    return 0.0;  // unreachable: n <= W <= GW
-  } else {
-    const int m = n - n % 8;  // end of the whole 8-blocks
-    double a = v;
-#pragma unroll
-    for (int b = 8; b < GW; b += 8) {
-      const double x = __shfl(v, (threadIdx.x + b) % GW, GW);  // v_{k+b} for lane k < 8
-      a = b < m ? a + x : a;
-    }
-    a = a + dpp_x<0>(a);
-    a = a + dpp_x<1>(a);
-    a = a + dpp_x<2>(a);
-    double r = __shfl(a, 0, GW);
-#pragma unroll
-    for (int i = 8; i < GW; i++) {
-      const double x = __shfl(v, i, GW);
-      r = (i >= m && i < n) ? r + x : r;
-    }
-    return r;
-  }
-}
+// (group_np_sum: kcommon.hpp)
 
 // step_b waves per SIMD the register budget is sized for: 5 (<= 96 VGPRs) leaves room on each SIMD
 // for a demand-kernel wave of the next step next to the four step_b waves of this one
@@ -1374,9 +1337,12 @@ __global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restri
 }
 #endif
 
-// (above 8 SKUs the K-wide register arrays of a lane need the larger budget of 2 waves per SIMD)
+// (above 8 SKUs the K-wide register arrays of a lane need the larger budget of 2 waves per SIMD; at
+// 9-16 warehouses, 4 envs per wave, the kernel runs few waves (C5: 2,048 for 8,192 envs, 2 per SIMD)
+// and 128 VGPRs keep its loop free of scratch spills, whose reloads wait on vmcnt(0), i.e. for the
+// record window in flight too)
 template <int K, int GW, bool DBG, bool TAB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : (GW >= 16 ? 4 : MSC_SB_WPE)))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int W = c.W, WK = W * K, R = c.R;
@@ -1551,6 +1517,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
   PROF_DECL(q_iter);
   PROF_DECL(q_nfin);
   PROF_T(q_t0);
+  // Software pipeline across orders: the next order's record (when it is in the same window) is read
+  // from LDS while this order allocates, and when its region differs from this one, that region's
+  // cost row is fetched at the end of this order, so it lands during the region epilogue instead of
+  // on the chain after it (global memory at C5's 256 regions x 16 warehouses; in-kernel counters:
+  // tools/prof_step_b.py)
+  uint4 nrec[NVR];
+  bool have_next = false;
+  int nreg = -1;
+  double ncof = 0.0, ncov = 0.0;
+  auto read_rec = [&](int q, uint4(&v)[NVR]) {
+#pragma unroll
+    for (int j = 0; j < NVR; j++) v[j] = win[((q / CH) & 1) * SB_REC + ((q % CH) * NVR + j) * EPW + myjj];
+  };
   for (int oi = 0; oi <= wmax; oi++) {
     if (oi > 0 && oi % CH == 0) {  // wave-uniform: window oi / CH is due, start the one after
       if (oi + CH <= wmax) {
@@ -1568,26 +1547,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
         uint4 v[NVR];
         uint16_t h[8 * NVR];
       } ur;
+      if (have_next) {
 #pragma unroll
-      for (int j = 0; j < NVR; j++) ur.v[j] = win[((oi / CH) & 1) * SB_REC + ((oi % CH) * NVR + j) * EPW + myjj];
+        for (int j = 0; j < NVR; j++) ur.v[j] = nrec[j];
+      } else {
+        read_rec(oi, ur.v);
+      }
+      have_next = oi + 1 < n_orders && (oi + 1) % CH != 0;
+      if (have_next) read_rec(oi + 1, nrec);
       if (oi < n_orders) r = ur.h[0];
 #pragma unroll
       for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
     }
+    // (prof build: the time of this block and its passes counted for the whole wave, i.e. also when
+    // only another env of the wave changes region)
+    PROF_T(q_f0);
+#ifdef MSC_PROF
+    PROF_ADD(q_nfin, __ballot(r != cur) != 0 ? 1ull : 0ull);
+#endif
     if (r != cur) {
-      PROF_T(q_f0);
       if (cur >= 0) finalize(cur);
-      PROF_ADD(q_fin, PROF_NOW() - q_f0);
-      PROF_ADD(q_nfin, 1);
       if (r >= 0 && wl) {
-        cof = cost_of(r);
-        cov = cost_ov(r);
+        if (r == nreg) {  // prefetched at the end of the previous order
+          cof = ncof;
+          cov = ncov;
+        } else {
+          cof = cost_of(r);
+          cov = cost_ov(r);
+        }
       }
       cur = r;
       lost_cnt = 0;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
     }
+    PROF_ADD(q_fin, PROF_NOW() - q_f0);
     if (oi == n_orders) continue;
     bool any_d = false;
     double tw = 0.0;
@@ -1597,7 +1591,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       any_d |= d[sk] > 0;
       tw += (double)d[sk] * skw[sk];
     }
-    if (!any_d) continue;  // an empty order ships nothing and is never lost
+    // the next order's region cost row, when its region differs (see above)
+    auto prefetch_costs = [&] {
+      if (have_next && wl) {
+        const int rn = (int)(nrec[0].x & 0xffffu);
+        if (rn != cur && rn != nreg) {
+          ncof = cost_of(rn);
+          ncov = cost_ov(rn);
+          nreg = rn;
+        }
+      }
+    };
+    if (!any_d) {  // an empty order ships nothing and is never lost
+      prefetch_costs();
+      continue;
+    }
     int rem[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
@@ -1693,6 +1701,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       u[sk] += rem[sk] > 0 ? rem[sk] : 0;
     }
     lost_cnt += anyrem ? 1 : 0;
+    prefetch_costs();
   }
   PROF_ADD(q_all, PROF_NOW() - q_t0);
   PROF_FLUSH(10, q_all);

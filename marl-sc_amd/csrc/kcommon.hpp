@@ -79,4 +79,43 @@ __device__ __forceinline__ double dpp_x(double v) {
   const int lo = dpp_x<S>((int)(b & 0xffffffffLL)), hi = dpp_x<S>((int)(b >> 32));
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+// numpy add.reduce order (pairwise_sum, n <= 128) of the group's lane values v_0..v_{n-1} without
+// materialising them: sequential below 8 (lane shuffles), else the eight strided accumulators
+// r_j = v_j + v_{j+8} + ... over the whole 8-blocks (lane j < 8 gathers its column), their tree as
+// 3 DPP butterfly steps over lanes 0..7 (IEEE addition is commutative, so the butterfly's pairs are
+// numpy's pairs), then the tail sequentially; the result reaches every lane of the group
+template <int GW>
+__device__ __forceinline__ double group_np_sum(double v, int n) {
+  if (n < 8) {
+    double r = 0.0;
+#pragma unroll
+    for (int j = 0; j < (GW < 8 ? GW : 8); j++) {
+      const double x = __shfl(v, j, GW);
+      r = j < n ? r + x : r;
+    }
+    return r;
+  }
+  if constexpr (GW < 8) {
+    return 0.0;  // unreachable: n <= GW
+  } else {
+    const int m = n - n % 8;  // end of the whole 8-blocks
+    double a = v;
+#pragma unroll
+    for (int b = 8; b < GW; b += 8) {
+      const double x = __shfl(v, (threadIdx.x + b) % GW, GW);  // v_{k+b} for lane k < 8
+      a = b < m ? a + x : a;
+    }
+    a = a + dpp_x<0>(a);
+    a = a + dpp_x<1>(a);
+    a = a + dpp_x<2>(a);
+    double r = __shfl(a, 0, GW);
+#pragma unroll
+    for (int i = 8; i < GW; i++) {
+      const double x = __shfl(v, i, GW);
+      r = (i >= m && i < n) ? r + x : r;
+    }
+    return r;
+  }
+}
+
 }  // namespace msc

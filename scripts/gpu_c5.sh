@@ -1,14 +1,14 @@
 #!/bin/bash
-# C5 / allocation-order A/B: GPU parity tests, then bench --config c5 with and without the
-# order-count sort of the group allocation kernel, and the C2 shape (Poisson, 4096 envs).
+# GPU tests and the C5 line alone (A/B of step_b changes). Stops at the first failure.
 set -u
+TAG=${1:-c5}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -n 2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-for cfg in ${AB_CFGS:-c5:1 c5:0 c2:1 c2:0 c5:1}; do
-  set -- ${cfg%:*} ${cfg#*:}
-  if [ "$1" = c5 ]; then args="--config c5"; else args="--envs 4096"; fi
-  MSC_ALLOC_SORT=$2 timeout -k 10 300 python bench.py $args --steps 200 --warmup 20 --no-cpu-baseline --rollout-T 0 > gpurun_out/ab_sort_$1_$2.log 2>&1 || exit $?
-  echo "$1 sort=$2 $(tail -n 1 gpurun_out/ab_sort_$1_$2.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["kernels_ms"])')"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 180 --timeout-method thread > gpurun_out/pytest_gpu_${TAG}.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -n 3 gpurun_out/pytest_gpu_${TAG}.log; [ $rc -eq 0 ] || exit $rc
+for rep in 1 2; do
+timeout -k 10 300 python bench.py --config c5 --steps 500 --warmup 50 --no-cpu-baseline > gpurun_out/bench_${TAG}_$rep.json.log 2>&1
+rc=$?; echo "c5 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+python3 -c "import json;d=[json.loads(l) for l in open('gpurun_out/bench_${TAG}_$rep.json.log') if l.startswith('{')][0];print('C5', round(d['value']/1e6,1), d['ms_per_step'], d['kernels_ms'])"
 done
+exit 0

@@ -590,14 +590,15 @@ def test_episode_ahead_memory_budget_binds_and_stays_exact(monkeypatch):
     b.check()
 
 
-@pytest.mark.parametrize("E", [1, 63, 1000])
-def test_scan_allocator_vs_oracle_sizes(monkeypatch, E):
+@pytest.mark.parametrize("E,W,K", [(1, 6, 4), (63, 6, 4), (1000, 6, 4), (63, 16, 5), (130, 13, 6), (70, 11, 2)])
+def test_scan_allocator_vs_oracle_sizes(monkeypatch, E, W, K):
     # the scan allocator (4 envs per block; a partial last block) and episode-ahead demand at odd
-    # env counts against the oracle, with max_splits limiting the warehouses per order
+    # env counts against the oracle, with max_splits limiting the warehouses per order; 9-16
+    # warehouses: 16-lane SKU groups, two SKU slots per lane above 4 SKUs
     monkeypatch.setenv("MSC_ALLOC_IMPL", "scan")
     monkeypatch.setenv("MSC_EA", "1")
-    cfg = make_synthetic_env_config(6, 20, 4, episode_length=5)
-    cfg["components"]["demand_allocator"]["params"]["max_splits"] = 1
+    cfg = make_synthetic_env_config(W, 20, K, episode_length=5)
+    cfg["components"]["demand_allocator"]["params"]["max_splits"] = 1 if W < 9 else 3
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     _lockstep(spec, E, 17, seed=E, check_every=2)
 
@@ -686,7 +687,7 @@ def test_episode_ahead_runtime_switch_stays_exact(monkeypatch):
 
 
 @pytest.mark.parametrize("lost", ["shipment", "cost", "closest"])
-@pytest.mark.parametrize("shape", [(8, 64, 5), (3, 7, 2)])
+@pytest.mark.parametrize("shape", [(8, 64, 5), (3, 7, 2), (16, 64, 5), (12, 9, 6), (9, 70, 3)])
 def test_scan_allocator_lost_sales_handlers_vs_oracle(monkeypatch, lost, shape):
     # the scan allocator's deferred lost-sales shares (shipment / cost softmax, flushed after the order
     # loop in region order; csrc/alloc_scan.hip flush_lost) and the inline closest handler, without
@@ -697,3 +698,32 @@ def test_scan_allocator_lost_sales_handlers_vs_oracle(monkeypatch, lost, shape):
     cfg = make_synthetic_env_config(W, R, K, episode_length=11, lost_sales=lost, initial_inventory=8)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     _lockstep(spec, 130, 24, seed=17, check_every=3)
+
+
+@pytest.mark.parametrize("W,K", [(16, 5), (10, 6)])
+def test_scan_allocator_wide_step_info_vs_group(monkeypatch, W, K):
+    # collect_step_info through the scan kernel's instrumented epilogue at 16-lane SKU groups (two
+    # slots per lane): every info key equal to the group kernel's on the same seeds (the golden
+    # fixtures pin the group kernel's infos to the reference at <= 8 warehouses)
+    cfg = make_synthetic_env_config(W, 12, K, episode_length=9, lost_sales="shipment", initial_inventory=15)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    outs = []
+    for impl in ("group", "scan"):
+        monkeypatch.setenv("MSC_ALLOC_IMPL", impl)
+        env = _vec(spec, 40, base_seed=5)
+        env.reset()
+        rng = np.random.default_rng(2)
+        rec = []
+        for t in range(12):
+            a = torch.from_numpy(rng.uniform(-1, 1, (40, W, K)).astype(np.float32)).cuda()
+            info = env.alloc_info()
+            env.step(a, info=info, want_f64=True)
+            rec.append({k: _np(v).copy() for k, v in info.items()} | {"rew": _np(env.rewards_f64).copy()})
+        env.check()
+        outs.append(rec)
+    for t, (g, sc) in enumerate(zip(*outs)):
+        for k in g:
+            if k in ("lost_sales", "costs", "rew"):
+                np.testing.assert_allclose(sc[k], g[k], rtol=0, atol=1e-9, err_msg=f"{k} t={t}")
+            else:
+                np.testing.assert_array_equal(sc[k], g[k], err_msg=f"{k} t={t}")
