@@ -1337,12 +1337,9 @@ __global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restri
 }
 #endif
 
-// (above 8 SKUs the K-wide register arrays of a lane need the larger budget of 2 waves per SIMD; at
-// 9-16 warehouses, 4 envs per wave, the kernel runs few waves (C5: 2,048 for 8,192 envs, 2 per SIMD)
-// and 128 VGPRs keep its loop free of scratch spills, whose reloads wait on vmcnt(0), i.e. for the
-// record window in flight too)
+// (above 8 SKUs the K-wide register arrays of a lane need the larger budget of 2 waves per SIMD)
 template <int K, int GW, bool DBG, bool TAB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : (GW >= 16 ? 4 : MSC_SB_WPE)))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int W = c.W, WK = W * K, R = c.R;
@@ -1517,19 +1514,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
   PROF_DECL(q_iter);
   PROF_DECL(q_nfin);
   PROF_T(q_t0);
-  // Software pipeline across orders: the next order's record (when it is in the same window) is read
-  // from LDS while this order allocates, and when its region differs from this one, that region's
-  // cost row is fetched at the end of this order, so it lands during the region epilogue instead of
-  // on the chain after it (global memory at C5's 256 regions x 16 warehouses; in-kernel counters:
-  // tools/prof_step_b.py)
-  uint4 nrec[NVR];
-  bool have_next = false;
-  int nreg = -1;
-  double ncof = 0.0, ncov = 0.0;
-  auto read_rec = [&](int q, uint4(&v)[NVR]) {
-#pragma unroll
-    for (int j = 0; j < NVR; j++) v[j] = win[((q / CH) & 1) * SB_REC + ((q % CH) * NVR + j) * EPW + myjj];
-  };
   for (int oi = 0; oi <= wmax; oi++) {
     if (oi > 0 && oi % CH == 0) {  // wave-uniform: window oi / CH is due, start the one after
       if (oi + CH <= wmax) {
@@ -1547,14 +1531,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
         uint4 v[NVR];
         uint16_t h[8 * NVR];
       } ur;
-      if (have_next) {
 #pragma unroll
-        for (int j = 0; j < NVR; j++) ur.v[j] = nrec[j];
-      } else {
-        read_rec(oi, ur.v);
-      }
-      have_next = oi + 1 < n_orders && (oi + 1) % CH != 0;
-      if (have_next) read_rec(oi + 1, nrec);
+      for (int j = 0; j < NVR; j++) ur.v[j] = win[((oi / CH) & 1) * SB_REC + ((oi % CH) * NVR + j) * EPW + myjj];
       if (oi < n_orders) r = ur.h[0];
 #pragma unroll
       for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
@@ -1568,13 +1546,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     if (r != cur) {
       if (cur >= 0) finalize(cur);
       if (r >= 0 && wl) {
-        if (r == nreg) {  // prefetched at the end of the previous order
-          cof = ncof;
-          cov = ncov;
-        } else {
-          cof = cost_of(r);
-          cov = cost_ov(r);
-        }
+        cof = cost_of(r);
+        cov = cost_ov(r);
       }
       cur = r;
       lost_cnt = 0;
@@ -1591,21 +1564,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       any_d |= d[sk] > 0;
       tw += (double)d[sk] * skw[sk];
     }
-    // the next order's region cost row, when its region differs (see above)
-    auto prefetch_costs = [&] {
-      if (have_next && wl) {
-        const int rn = (int)(nrec[0].x & 0xffffu);
-        if (rn != cur && rn != nreg) {
-          ncof = cost_of(rn);
-          ncov = cost_ov(rn);
-          nreg = rn;
-        }
-      }
-    };
-    if (!any_d) {  // an empty order ships nothing and is never lost
-      prefetch_costs();
-      continue;
-    }
+    if (!any_d) continue;  // an empty order ships nothing and is never lost
     int rem[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
@@ -1701,7 +1660,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       u[sk] += rem[sk] > 0 ? rem[sk] : 0;
     }
     lost_cnt += anyrem ? 1 : 0;
-    prefetch_costs();
   }
   PROF_ADD(q_all, PROF_NOW() - q_t0);
   PROF_FLUSH(10, q_all);
