@@ -127,6 +127,21 @@ def test_config_validation_rejects_bad_values():
         validate_environment_config(bad, allow_nr_ne_nw=True)
 
 
+def test_shape_caps_agree_across_header_abi_spec():
+    # include/marlsc.h caps (32 warehouses x 16 SKUs x 4,096 regions) = the Python mirror's = what the
+    # spec accepts; one past them is rejected before any device call
+    import re
+    from marlsc import EnvSpec, abi, make_synthetic_env_config
+    hdr = (REPO / "include" / "marlsc.h").read_text()
+    caps = {k: int(re.search(rf"#define MSC_MAX_{k} (\d+)", hdr).group(1)) for k in ("W", "K", "R")}
+    assert (caps["W"], caps["K"], caps["R"]) == (abi.MAX_W, abi.MAX_K, abi.MAX_R) == (32, 16, 4096)
+    spec = EnvSpec.from_config(make_synthetic_env_config(32, 6, 16), {"include_warehouse_id": True})
+    assert (spec.W, spec.K) == (32, 16)
+    for W, K in ((33, 4), (4, 17)):
+        with pytest.raises(ValueError):
+            EnvSpec.from_config(make_synthetic_env_config(W, 6, K), {"include_warehouse_id": True})
+
+
 def test_seed_manager_semantics():
     from marlsc import SeedManager
     sm = SeedManager(42)
