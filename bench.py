@@ -6,8 +6,9 @@ A "step" = one pass of msc_env_step over every env of the rank (demand generatio
 fused step kernel, including in-kernel auto-resets every episode_length steps), with synthetic
 uniform[-1, 1] actions already resident in HBM. Metric: agent-steps/s = envs x agents x steps / s,
 whole job. N > 1: one process per GPU (torchrun), each rank owns `--envs` envs with disjoint global
-env ids (weak scaling, no data-path collective); barrier + synchronize bracket the timed region
-and the max over ranks is reported.
+env ids (weak scaling, no data-path collective: the headline), and the line's `strong` object times
+BASELINE configs[3] as stated, 32,768 envs in total split over the ranks (`--scaling`); barrier +
+synchronize bracket every timed region and the max over ranks is reported.
 
 Roofline: average device duration of each kernel measured with HIP events on the launch stream
 (torch's current stream); algorithmic bytes per launch from the state layout.
@@ -43,8 +44,11 @@ def valu_peak(clk_mhz: float = CLOCK_MAX_MHZ) -> float:
 
 VALU_PEAK_WINST = valu_peak()
 # secondary, measured (tools/ubench_isa.hip, profiles/r02/ubench_isa.txt): independent v_add_u32 at
-# 4 waves per SIMD retired one wave64 instruction per 1.78 ns per SIMD = 574 G/s for the chip at the
-# (unrecorded) clock of that run; f64 mul / 64-bit mad: 1.35-1.7x the cost of a v_add_u32
+# 4 waves per SIMD retired one wave64 instruction per 1.78 ns per SIMD = 574 G/s for the chip. The
+# same run's shader-cycle counter (s_memtime) reads 8.70 cycles per instruction per wave at 4 waves,
+# i.e. one issue per 2.17 cycles per SIMD: the 2-cycle basis above, at an effective ~1.2 GHz over that
+# run's wall time (launch ramp and clock under an all-CU load included), so the two peaks differ by
+# the clock, not by the cycles per instruction; f64 mul / 64-bit mad: 1.35-1.7x a v_add_u32
 VALU_UBENCH_WINST = 1024 / 1.784e-9
 
 
@@ -56,7 +60,9 @@ def issue_object(insts: float, seconds: float, clk_mhz=None, **extra) -> dict:
     o.update({"bound": "valu issue", "achieved": round(ach / 1e9, 2), "peak": round(VALU_PEAK_WINST / 1e9, 1),
               "unit": "G wave-instructions/s", "frac": round(ach / VALU_PEAK_WINST, 4),
               "peak_basis": "1024 SIMDs x 2400 MHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md:34,54)",
-              "ubench_peak": round(VALU_UBENCH_WINST / 1e9, 1)})
+              "ubench_peak": round(VALU_UBENCH_WINST / 1e9, 1),
+              "ubench_basis": "tools/ubench_isa.hip: 2.17 shader cycles per v_add_u32 issue per SIMD at 4 waves "
+                              "(the 2-cycle basis), 1.78 ns wall per issue (~1.2 GHz effective over the run)"})
     if clk_mhz:
         pk = valu_peak(clk_mhz)
         o.update({"clock_mhz": clk_mhz, "peak_at_clock": round(pk / 1e9, 1), "frac_at_clock": round(ach / pk, 4)})
@@ -120,6 +126,7 @@ def time_env(env, pool, steps: int, warmup: int, world: int, ea: bool = False):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    w0 = env.work_counters()
     t0 = time.perf_counter()
     for i in range(steps):
         env.step(pool[i % len(pool)])
@@ -128,6 +135,7 @@ def time_env(env, pool, steps: int, warmup: int, world: int, ea: bool = False):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    w1 = env.work_counters()
     env.check()
     # the timing pass: 50 steps, or with episode-ahead demand 2.5 episodes (a generation launch covers
     # whole episodes of every env: one or two per episode in steady state)
@@ -153,30 +161,52 @@ def time_env(env, pool, steps: int, warmup: int, world: int, ea: bool = False):
     torch.cuda.synchronize()
     tm["host_ms_per_step"] = tb / nb * 1e3
     tm["enqueue_ms_per_step"] = t_host / steps * 1e3
+    tm["window"] = window_work(w0, w1, env.n_envs, steps)
     env.check()
     return dt, tm
 
 
-def time_rollout(envs, module, T: int, world: int, seed: int, warm: int = 1, reps: int = 1):
+def window_work(w0: dict, w1: dict, n_envs: int, steps: int) -> dict:
+    """Demand work issued (and, after the window's closing synchronize, finished) inside a timed
+    window, from the library's monotonic counters (msc_env_work_counters): episode-ahead generation
+    launches and the env-steps of demand they drew, per-step demand launches (E env-steps each),
+    against the env-steps the window timed. In steady state the generated env-steps cover the timed
+    ones (the generation runs up to S episodes ahead, so a window can also hold demand its own steps
+    do not read yet)."""
+    ea_l = int(w1["ea_launches"] - w0["ea_launches"])
+    ea_w = int(round(w1["ea_env_steps"] - w0["ea_env_steps"]))
+    dl = int(w1["demand_launches"] - w0["demand_launches"])
+    return {"ea_launches_in_window": ea_l, "ea_env_steps_in_window": ea_w, "demand_launches_in_window": dl,
+            "demand_env_steps_in_window": ea_w + dl * n_envs, "env_steps_timed": int(n_envs) * int(steps),
+            "steps_in_window": int(w1["steps"] - w0["steps"])}
+
+
+def time_rollout(envs, module, T: int, world: int, seed: int, warm: int = 1, reps: int = 1, with_window: bool = False):
     """Seconds per rollout of T steps (RolloutCollector.collect) after `warm` untimed ones."""
     import torch
     import torch.distributed as dist
     from marlsc.rollout import RolloutCollector
     col = RolloutCollector(envs, module, T, seed=seed)
+    el = envs if isinstance(envs, list) else [envs]
     for _ in range(warm):
         col.collect()  # warm-up (GEMM heuristics, allocator; episode-ahead demand reaches steady state)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    w0 = [x.work_counters() for x in el]
     t0 = time.perf_counter()
     for _ in range(reps):
         col.collect()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    for x in (envs if isinstance(envs, list) else [envs]):
+    dt = (time.perf_counter() - t0) / reps
+    ww = [window_work(a, x.work_counters(), x.n_envs, T * reps) for a, x in zip(w0, el)]
+    for x in el:
         x.check()
-    return (time.perf_counter() - t0) / reps
+    if with_window:
+        return dt, {k: sum(w[k] for w in ww) for k in ww[0]}
+    return dt
 
 
 def c2_line(args, rank: int):
@@ -219,7 +249,7 @@ def c2_line(args, rank: int):
     # while no generation launch is in flight and ~0.34 while one is (the launches of one refill take
     # most of the next 4 rollouts), so a window of one or two periods read 0.21-0.29 ms per step
     # depending on its phase (profiles/r04/c2_rollout_phases.txt); 16 rollouts average the phases
-    t_roll = time_rollout(env, module, T, 1, seed=rank, warm=4, reps=16) if args.rollout_T > 0 else 0.0
+    t_roll, roll_win = time_rollout(env, module, T, 1, seed=rank, warm=4, reps=16, with_window=True) if args.rollout_T > 0 else (0.0, None)
     a_h, c_h = rc.actor["hidden_sizes"], rc.critic["hidden_sizes"]
     out = {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x {spec.K} SKUs "
                        f"(BASELINE configs[1])",
@@ -230,7 +260,8 @@ def c2_line(args, rank: int):
                       f"generated in 50-step chunks, several slots per launch)" if tm["slots"] else "per step (pipelined)"),
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
                           "demand_ea_chunk": round(tm["ea_ms"], 4) if tm["n_ea"] else None,
-                          "demand_per_step": round(tm["demand_ms"], 4) if tm["n_demand"] else None}}
+                          "demand_per_step": round(tm["demand_ms"], 4) if tm["n_demand"] else None},
+           "window": tm["window"]}
     # the step kernels against the VALU issue peak: PMC instruction counts of the same workload
     # (scripts/gpu_profile.sh -> profiles/traffic.json) over the live step-kernel time
     tj = Path(args.traffic_json)
@@ -256,7 +287,8 @@ def c2_line(args, rank: int):
                                     f"{'-'.join(map(str, a_h))}-{spec.K}, critic {spec.local_obs_dim}-"
                                     f"{'-'.join(map(str, c_h))}-1 on local obs, fp32, parameter sharing",
                           "includes": "env step, actor + critic forward, Gaussian sampling, buffer writes, truncation "
-                                      "bootstrap, GAE kernel, adv-norm statistics + normalise"}
+                                      "bootstrap, GAE kernel, adv-norm statistics + normalise",
+                          "window": roll_win}
     env.close()
     return out
 
@@ -292,7 +324,7 @@ def c5_line(args, rank: int):
            "value": round(E * spec.W * steps / dt, 1), "unit": "agent-steps/s", "ms_per_step": round(dt / steps * 1e3, 4),
            "steps": steps, "warmup": args.warmup, "obs_normalization": meta.get("obs_normalization", "off"),
            "host_ms_per_step": round(tm["host_ms_per_step"], 4), "enqueue_ms_per_step": round(tm["enqueue_ms_per_step"], 4),
-           "kernels_ms": {"step_kernels": round(tm["step_ms"], 4)}}
+           "kernels_ms": {"step_kernels": round(tm["step_ms"], 4)}, "window": tm["window"]}
     # the step kernels (no demand kernel: the trace window is read inside step_a) against the VALU
     # issue peak and their HBM bytes, from the PMC passes of this workload (profiles/traffic.json)
     tj = Path(args.traffic_json)
@@ -308,6 +340,69 @@ def c5_line(args, rank: int):
                 sum(cn), tm["step_ms"] * 1e-3, None, kernel="step_kernels (" + " + ".join(names) + ")",
                 insts_per_step=int(sum(cn)), traffic=sum(tb) if all(x is not None for x in tb) else None,
                 note="the allocation is one env per lane group on the per-order argmin chain (DESIGN.md section 3)")
+    return out
+
+
+def strong_line(args, rank: int, world: int, spec, meta: dict) -> dict:
+    """BASELINE configs[3] as stated: `--strong-envs` envs in total (32,768) sharded over the N ranks,
+    rank g owning global env ids [g * E / N, (g + 1) * E / N) (every env seeded from
+    its global id, so the trajectories are those of the one-GPU run). Per rank the library picks its
+    kernels by shard size (per-step pipelined demand + lane allocator at >= 16,384 envs, episode-ahead
+    demand + scan allocator at <= 8,192), as a one-GPU run of that size would. Barrier + synchronize
+    bracket the window, max over ranks; then the MAPPO rollout over the same shards (the adv-norm
+    statistics all-reduced across ranks each rollout)."""
+    import torch
+    import torch.distributed as dist
+    from marlsc.seeding import default_train_seed
+    from marlsc.vec_env import VecInventoryEnv
+    E_tot = args.strong_envs
+    if E_tot % world:
+        raise SystemExit(f"--strong-envs {E_tot} is not divisible by {world} ranks")
+    n = E_tot // world
+    env = VecInventoryEnv(None, n, spec=spec, device=torch.cuda.current_device(), base_seed=default_train_seed(42),
+                          env_index_offset=rank * n)
+    g = torch.Generator(device="cuda").manual_seed(4321 + rank)
+    pool = [torch.rand((n, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
+    env.reset()
+    T = spec.episode_length
+    ea = bool(env.ea_slots)
+    if ea:  # whole refill periods after the generation pipeline has filled (as the c2 line)
+        period = 4 * T
+        steps, warm = max(6 * period, -(-args.steps // period) * period), 6 * period
+    else:
+        steps, warm = args.steps, args.warmup
+    dt, tm = time_env(env, pool, steps, warm, world, ea=ea)
+    t_roll, roll_win = 0.0, None
+    if args.rollout_T > 0:
+        import yaml
+        from marlsc.rollout import ActorCritic, RolloutConfig
+        rc = RolloutConfig.from_algorithm_config(yaml.safe_load(open(REPO / "config_files/algorithms/mappo.yaml")))
+        torch.manual_seed(0)
+        module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
+        env.set_pipelining(True)
+        t_roll, roll_win = time_rollout(env, module, args.rollout_T, world, seed=0, warm=4 if ea else 1,
+                                        reps=8 if ea else 2, with_window=True)
+    tt = torch.tensor([dt, t_roll], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt, t_roll = (float(x) for x in tt.tolist())
+    env.close()
+    out = {"workload": f"InventoryEnvironment.step x {E_tot} envs in total ({n} per GPU x {world}), {spec.W} agents x "
+                       f"{spec.R} regions x {spec.K} SKUs (BASELINE configs[3])",
+           "scaling": "strong", "n_envs_total": E_tot, "n_envs_per_gpu": n, "n_gpus": world,
+           "value": round(E_tot * spec.W * steps / dt, 1), "unit": "agent-steps/s",
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warm,
+           "env_ids": f"rank g owns global env ids [g*{n}, (g+1)*{n})",
+           "demand": "episode-ahead" if ea else "per step (pipelined)",
+           "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
+                          "demand_per_step": round(tm["demand_ms"], 4) if tm["n_demand"] else None,
+                          "demand_ea_chunk": round(tm["ea_ms"], 4) if tm["n_ea"] else None},
+           "window": tm["window"]}
+    if args.rollout_T > 0:
+        out["rollout"] = {"value": round(E_tot * spec.W * args.rollout_T / t_roll, 1), "unit": "agent-steps/s",
+                          "ms_per_step": round(t_roll / args.rollout_T * 1e3, 4), "T": args.rollout_T,
+                          "policy": "MAPPO (config_files/algorithms/mappo.yaml), adv-norm statistics all-reduced over ranks",
+                          "window": roll_win}
     return out
 
 
@@ -363,6 +458,11 @@ def main():
     ap.add_argument("--c5-envs", type=int, default=8192, help="envs of the configs[4] line (0 = skip it)")
     ap.add_argument("--no-ea-line", dest="ea_line", action="store_false",
                     help="skip the episode-ahead steady-state line of the headline envs")
+    ap.add_argument("--scaling", choices=("weak", "strong", "both"), default="both",
+                    help="N > 1: weak = each rank steps --envs envs (global ids [g*E, (g+1)*E)); strong = BASELINE "
+                         "configs[3], --strong-envs in total split over the ranks; both (default) = the weak headline "
+                         "plus a `strong` object (at N = 1 the two coincide and only the headline runs)")
+    ap.add_argument("--strong-envs", type=int, default=32768, help="total envs of the strong-scaling measurement")
     ap.add_argument("--obs-norm", choices=("meanstd_custom", "off"), default="meanstd_custom",
                     help="observation normalisation of the headline env (the reference MAPPO config's is meanstd_custom)")
     ap.add_argument("--rollout-lanes", type=int, default=int(os.environ.get("MSC_ROLLOUT_LANES", "1")),
@@ -449,6 +549,7 @@ def main():
                    "kernels_ms": {"step_kernels": round(tm_ea["step_ms"], 4),
                                   DEMAND_KERNEL + "_ea": round(tm_ea["ea_ms"], 3),
                                   "ea_env_steps_per_launch": int(tm_ea["ea_env_steps_per_launch"])},
+                   "window": tm_ea["window"],
                    "note": "episode-ahead demand in steady state (msc_env_set_episode_ahead): one generation launch "
                            "per episode refills a slot with a whole future episode of every env; the headline "
                            "`value` is the per-step pipelined path, whose first steps the driver's short "
@@ -461,7 +562,7 @@ def main():
     ea_work = tm["ea_env_steps_per_launch"] if ea_regime else 0.0
     # (3) MAPPO rollout (configs[2]): env step + actor/critic forward + sampling + buffer writes +
     #     GAE kernel + adv-norm statistics all-reduce, T steps per rollout
-    t_roll = 0.0
+    t_roll, roll_win = 0.0, None
     if args.rollout_T > 0:
         import yaml
         from marlsc.rollout import ActorCritic, RolloutCollector, RolloutConfig
@@ -479,7 +580,7 @@ def main():
             for x in renv:
                 x.set_pipelining(os.environ.get("MSC_ROLLOUT_PIPELINE", "1") != "0")
                 x.reset()
-        t_roll = time_rollout(renv, module, args.rollout_T, world, seed=0)
+        t_roll, roll_win = time_rollout(renv, module, args.rollout_T, world, seed=0, with_window=True)
     # (4) the HBM-bound kernel of the rollout: msc_gae (GAE reverse scan + advantage statistics) over
     #     one MAPPO rollout's [T, E * W] sequences, timed alone with events on its stream
     gae_line = None
@@ -541,6 +642,11 @@ def main():
                         "shape": f"actor {spec.local_obs_dim}-{H1}-{H2}-{spec.K} over N={N} rows (E x W of one rollout step), "
                                  f"f32 MFMA, timed alone"}
             del xg, yo
+    # (6) N > 1: BASELINE configs[3] as stated, the same 32,768 envs split over the ranks (strong)
+    strong = None
+    if world > 1 and args.scaling in ("strong", "both") and args.config == "c3":
+        env.close()
+        strong = strong_line(args, rank, world, spec, meta)
     c2 = None
     if world == 1 and args.c2_envs > 0 and args.config == "c3":
         env.close()
@@ -612,6 +718,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            "window": tm["window"],
             "dtype": "int32 state, u64 PCG64, f64 rewards, f32 obs",
             "data": ("synthetic (SURVEY.md 8(d) cost structure, Poisson demand lambda_o=4 p=0.667 lambda_q=5, uniform[-1,1] actions)"
                      if args.config == "c3" else
@@ -652,7 +759,8 @@ def main():
                           f"obs {meta.get('obs_normalization', 'off')}",
                 "lanes": max(1, args.rollout_lanes),
                 "includes": "env step (envs split into `lanes` handles on their own HIP streams), actor forward, MAPPO critic on local||global (first layer split: global block once per env), Gaussian sampling, "
-                            "buffer writes, truncation bootstrap, GAE kernel, adv-norm all-reduce + normalise"}
+                            "buffer writes, truncation bootstrap, GAE kernel, adv-norm all-reduce + normalise",
+                "window": roll_win}
         if ea_line is not None:
             b_dem_ea = algorithmic_bytes(spec, mean_orders)[0]
             w_ea = ea_line["kernels_ms"]["ea_env_steps_per_launch"]
@@ -670,6 +778,14 @@ def main():
                     if ci:
                         ea_line["roofline"]["valu_issue"] = issue_object(ci, t_l, None, insts_per_launch=int(ci))
             out["episode_ahead"] = ea_line
+        if strong is not None:
+            out["strong"] = strong
+            if args.scaling == "strong":  # the headline is configs[3] as stated
+                out["weak"] = {"value": out["value"], "ms_per_step": out["ms_per_step"], "n_envs_per_gpu": E}
+                out.update({"value": strong["value"], "ms_per_step": strong["ms_per_step"], "steps": strong["steps"],
+                            "warmup": strong["warmup"], "scaling": "strong"})
+                out["config"]["n_envs_per_gpu"] = strong["n_envs_per_gpu"]
+                out["config"]["workload"] = strong["workload"]
         if c2 is not None:
             out["c2"] = c2
         if c5 is not None:

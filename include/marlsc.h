@@ -50,6 +50,7 @@ typedef struct ihipStream_t* msc_stream_t; /* == hipStream_t */
 #define MSC_MAX_K 16   /* SKUs (above 8: the sequential demand sampler and the group allocator) */
 #define MSC_MAX_R 4096 /* demand regions */
 #define MSC_HISTORY 5  /* rolling window, multi_env.py:147 */
+#define MSC_ORDER_CAP_MAX (1 << 24) /* Poisson order records per env and step: sum(lambda_orders) + 12 sqrt(.) + 64 */
 
 /* Component `type` strings of the reference's registries (src/environment/registry.py:300-308). */
 enum msc_demand_type   { MSC_DEMAND_POISSON = 0, MSC_DEMAND_EMPIRICAL = 1 };
@@ -238,6 +239,13 @@ int msc_env_read_timing(msc_env* env, double* demand_ms, double* step_ms, int64_
  * env-steps of demand one timed launch generated (slots x steps x envs; for roofline accounting). */
 int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* slots, int32_t* active,
                            double* env_steps_per_launch);
+
+/* Demand work issued by the handle since create (monotonic; differences bracket a timed window):
+ * episode-ahead generation launches (chunks) and the env-steps of demand they drew, per-step demand
+ * launches (E env-steps each), and msc_env_step calls. Everything issued before a device-wide
+ * synchronize has finished after it. */
+int msc_env_work_counters(const msc_env* env, int64_t* ea_launches, double* ea_env_steps, int64_t* demand_launches,
+                          int64_t* steps);
 
 /* Episode-ahead memory of the handle: the budget computed at create time (bytes; 0 when EA was not
  * requested) and the bytes allocated for the slots (0: EA off). */

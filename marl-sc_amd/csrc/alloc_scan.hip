@@ -451,23 +451,35 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
       const double2 t = tab_at(rr, ww);
       cst[ww] = t.x + t.y * tw;
     }
-    // rank of a = the warehouses that sort before it; 32-bit counters per warehouse (a 64-bit
-    // packed sum of 120 selected constants at 16 warehouses ran out of registers)
-    int rk[GW];
-#pragma unroll
-    for (int a = 0; a < GW; a++) rk[a] = a < W ? 0 : a;
-#pragma unroll
-    for (int a = 0; a < GW; a++)
-#pragma unroll
-      for (int b = a + 1; b < GW; b++)
-        if (b < W) {
-          const bool lt = cst[b] < cst[a];
-          rk[a] += lt ? 1 : 0;
-          rk[b] += lt ? 0 : 1;
-        }
     Rho rho = 0;
+    if constexpr (GW <= 8) {
+      // up to 8 warehouses: the 4-bit ranks as one packed 32-bit sum (one select + add per pair)
 #pragma unroll
-    for (int a = 0; a < GW; a++) rho |= (Rho)rk[a] << (4 * a);
+      for (int a = 0; a < GW; a++)
+#pragma unroll
+        for (int b = a + 1; b < GW; b++)
+          if (b < W) rho += cst[b] < cst[a] ? (1u << (4 * a)) : (1u << (4 * b));
+#pragma unroll
+      for (int ww = 0; ww < GW; ww++)
+        if (ww >= W) rho |= (Rho)ww << (4 * ww);
+    } else {
+      // rank of a = the warehouses that sort before it; 32-bit counters per warehouse (a 64-bit
+      // packed sum of 120 selected constants at 16 warehouses ran out of registers)
+      int rk[GW];
+#pragma unroll
+      for (int a = 0; a < GW; a++) rk[a] = a < W ? 0 : a;
+#pragma unroll
+      for (int a = 0; a < GW; a++)
+#pragma unroll
+        for (int b = a + 1; b < GW; b++)
+          if (b < W) {
+            const bool lt = cst[b] < cst[a];
+            rk[a] += lt ? 1 : 0;
+            rk[b] += lt ? 0 : 1;
+          }
+#pragma unroll
+      for (int a = 0; a < GW; a++) rho |= (Rho)rk[a] << (4 * a);
+    }
     return rho;
   };
 

@@ -93,6 +93,10 @@ struct msc_env {
   hipEvent_t ev_gen[MSC_EA_MAX_S] = {}, ev_cons[MSC_EA_MAX_S] = {}, ev_snap = nullptr;
   std::vector<hipEvent_t> tev_ea;  // timing of EA launches (msc_env_set_timing)
   std::vector<double> tea_work;    // env-steps generated by each timed EA launch
+  // demand work issued since create (msc_env_work_counters): episode-ahead generation launches
+  // (chunks) and the env-steps of demand they draw; per-step demand launches (E env-steps each); steps
+  int64_t cnt_ea_launch = 0, cnt_dem_launch = 0, cnt_steps = 0;
+  double cnt_ea_work = 0.0;
   int n_tea = 0;
 };
 
@@ -134,6 +138,8 @@ static hipError_t ea_launch_chunk(msc_env* env, const EaLaunch& l) {
   }
   hipError_t e = launch_demand_ea(env->c, env->dev, l, es);
   if (e != hipSuccess) return e;
+  env->cnt_ea_launch++;
+  env->cnt_ea_work += (double)l.nslots * (double)(l.t1 - l.t0) * (double)env->c.E;
   if (tm) (void)hipEventRecord(env->tev_ea[2 * env->n_tea++ + 1], es);
   if (l.t1 >= env->c.T) {
     for (int k = 0; k < l.nslots; k++) {
@@ -364,7 +370,14 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
         if (lq >= 10.0) c.demand_ptrs = 1;
       }
     }
-    order_cap = (int)ceil(lam_sum + 12.0 * sqrt(lam_sum + 1.0) + 64.0);
+    // record capacity per env and step in int64 first: the kernels index records with int32, so a
+    // configuration whose per-step capacity does not fit is rejected here (rates up to 1e6 x 4,096
+    // regions would otherwise wrap the cast)
+    const double cap_d = ceil(lam_sum + 12.0 * sqrt(lam_sum + 1.0) + 64.0);
+    if (!(cap_d <= (double)MSC_ORDER_CAP_MAX))
+      return set_err(-1, "sum of lambda_orders %g: per-step order capacity %.0f exceeds %d records per env", lam_sum,
+                     cap_d, MSC_ORDER_CAP_MAX);
+    order_cap = (int)cap_d;
     // equal parameters in every region (and SKU): the demand parser's constant-threshold variant
     c.demand_uni = 1;
     for (int r = 0; r < R; r++) {
@@ -478,11 +491,26 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       if (const char* es = getenv("MSC_EA_SLOTS")) S = atoi(es);
       S = S < 2 ? 2 : (S > MSC_EA_MAX_S ? MSC_EA_MAX_S : S);
       if (want) {
-        double lam_sum = 0.0;
-        for (int r = 0; r < R; r++) lam_sum += d->lambda_orders[r];
+        double lam_sum = 0.0, draws = 0.0;
+        // expected uniforms per Poisson draw: lambda + 1 for the multiplication method, a few per
+        // PTRS trial (two uniforms, acceptance > 0.5) at lambda >= 10
+        auto per_draw = [](double lam) { return lam < 10.0 ? lam + 1.0 : 8.0; };
+        for (int r = 0; r < R; r++) {
+          const double lo = d->lambda_orders[r];
+          lam_sum += lo;
+          double per_order = K;  // the SKU mask's Bernoulli draws
+          for (int s = 0; s < K; s++) per_order += d->probability_skus[r] * per_draw(d->lambda_quantity[(size_t)r * K + s]);
+          draws += per_draw(lo) + lo * per_order;
+        }
         const double m = lam_sum * d->episode_length;
-        c.ea_S = S;
-        c.ea_cap = (int64_t)ceil(m + 12.0 * sqrt(m + 1.0) + 64.0);
+        draws *= d->episode_length;
+        const double cap_d = ceil(m + 12.0 * sqrt(m + 1.0) + 64.0);
+        // slot record indices are int32 in the kernels and stream positions uint32: an episode whose
+        // records or draws (with a 12-sigma margin) do not fit keeps per-step demand
+        if (cap_d * nv <= (double)INT32_MAX && draws + 12.0 * sqrt(draws + 1.0) < 4294967295.0) {
+          c.ea_S = S;
+          c.ea_cap = (int64_t)cap_d;
+        }
       }
     }
   }
@@ -887,12 +915,14 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
     } else {
       HIP_TRY(tmark(env, env->tev_dem, env->n_tdem, 0, st));
       HIP_TRY(launch_demand(c, env->dev + b, st));
+      env->cnt_dem_launch++;
       HIP_TRY(tmark(env, env->tev_dem, env->n_tdem++, 1, st));
       HIP_TRY(hipEventRecord(env->ev_dem[b], st));
     }
   }
   HIP_TRY(tmark(env, env->tev_step, env->n_tstep, 0, st));
   HIP_TRY(launch_step(c, env->dev + b, io, false, st));
+  env->cnt_steps++;
   HIP_TRY(tmark(env, env->tev_step, env->n_tstep++, 1, st));
   HIP_TRY(hipEventRecord(env->ev_step[b], st));
   env->ready[b] = false;
@@ -918,6 +948,7 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
     HIP_TRY(hipStreamWaitEvent(env->side, env->ev_reset, 0));
     HIP_TRY(tmark(env, env->tev_dem, env->n_tdem, 0, env->side));
     HIP_TRY(launch_demand(c, env->dev + nb, env->side));
+    env->cnt_dem_launch++;
     HIP_TRY(tmark(env, env->tev_dem, env->n_tdem++, 1, env->side));
     HIP_TRY(hipEventRecord(env->ev_dem[nb], env->side));
     env->ready[nb] = true;
@@ -1038,6 +1069,16 @@ int msc_env_read_timing_ea(msc_env* env, double* ea_ms, int64_t* n_ea, int32_t* 
   return 0;
 }
 
+int msc_env_work_counters(const msc_env* env, int64_t* ea_launches, double* ea_env_steps, int64_t* demand_launches,
+                          int64_t* steps) {
+  if (!env) return set_err(-1, "null env");
+  if (ea_launches) *ea_launches = env->cnt_ea_launch;
+  if (ea_env_steps) *ea_env_steps = env->cnt_ea_work;
+  if (demand_launches) *demand_launches = env->cnt_dem_launch;
+  if (steps) *steps = env->cnt_steps;
+  return 0;
+}
+
 int msc_env_generate_demand(msc_env* env, msc_stream_t stream) {
   if (!env) return set_err(-1, "null env");
   if (env->c.demand_type != MSC_DEMAND_POISSON) return 0;
@@ -1050,6 +1091,7 @@ int msc_env_generate_demand(msc_env* env, msc_stream_t stream) {
   HIP_TRY(hipStreamWaitEvent(st, env->ev_dem[b ^ 1], 0));  // last advance of the demand streams
   HIP_TRY(hipStreamWaitEvent(st, env->ev_reset, 0));
   HIP_TRY(launch_demand(env->c, env->dev + b, st));
+  env->cnt_dem_launch++;
   HIP_TRY(hipEventRecord(env->ev_dem[b], st));
   env->ready[b] = true;
   return 0;

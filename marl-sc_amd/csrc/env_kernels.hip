@@ -1908,16 +1908,14 @@ size_t demand_lds_bytes(const EnvConst& c) {
 #endif
 
 template <int K, int G>
-static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea) {
+static hipError_t launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea) {
   using DFn = void (*)(const DevEnv*);
   using UFn = void (*)(const DevEnv*, EaLaunch);
   if (c.demand_ptrs) {  // a rate >= 10: numpy's PTRS branch, the sequential sampler (demand_ab.hip)
-    (void)launch_demand_seq(c, d, st, ea);
-    return;
+    return launch_demand_seq(c, d, st, ea);
   }
   if (G == 3 && c.demand_impl == 7 && demand_ab_supported(c)) {  // the split parser (demand_ab.hip, A/B)
-    (void)launch_demand_ab(c, d, st, ea);
-    return;
+    return launch_demand_ab(c, d, st, ea);
   }
   const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
   const bool t = park_lds_tables(c);
@@ -1927,41 +1925,43 @@ static void launch_split_demand(const EnvConst& c, const DevEnv* d, hipStream_t 
                                 : (t ? (UFn)demand_unit_kernel<K, G, true, false, true> : (UFn)demand_unit_kernel<K, G, false, false, true>);
     const size_t lds_u = unit_lds_fixed() + (t && !c.demand_uni ? tab : 0);
     hipLaunchKernelGGL(fn, grid_for((int64_t)ea->nslots * c.E, c.epw_dem), dim3(BS * (1 + G)), lds_u, st, d, *ea);
-    return;
+    return hipGetLastError();
   }
   if (c.demand_impl == 5) {  // 4-draw parking parser (A/B: MSC_DEMAND_IMPL=park4)
     const DFn fn = t ? (DFn)demand_park4_kernel<K, G, true> : (DFn)demand_park4_kernel<K, G, false>;
     hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), lds, st, d);
-    return;
+    return hipGetLastError();
   }
   const UFn fn = c.demand_uni ? (UFn)demand_unit_kernel<K, G, false, true, false>
                               : (t ? (UFn)demand_unit_kernel<K, G, true, false, false> : (UFn)demand_unit_kernel<K, G, false, false, false>);
   hipLaunchKernelGGL(fn, grid_for(c.E, c.epw_dem), dim3(BS * (1 + G)), lds, st, d, EaLaunch{0, 0, 0, 0, 0, 0, 0});
+  return hipGetLastError();
 }
 
 template <int K>
-static void launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea = nullptr) {
+static hipError_t launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea = nullptr) {
   if constexpr (K > 8) {  // above 8 SKUs: the sequential sampler (demand_ab.hip), per step or episode-ahead
-    (void)launch_demand_seq(c, d, st, ea);
+    return launch_demand_seq(c, d, st, ea);
   } else if (c.demand_gen == 1) {
-    launch_split_demand<K, 1>(c, d, st, ea);
+    return launch_split_demand<K, 1>(c, d, st, ea);
   } else if (c.demand_gen == 2) {
-    launch_split_demand<K, 2>(c, d, st, ea);
+    return launch_split_demand<K, 2>(c, d, st, ea);
   } else {
-    launch_split_demand<K, 3>(c, d, st, ea);
+    return launch_split_demand<K, 3>(c, d, st, ea);
   }
 }
 
 hipError_t MSC_EK_FN(launch_demand)(const EnvConst& c, const DevEnv* d, hipStream_t st) {
-  MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st), return launch_demand_w1(c, d, st), return launch_demand_w2(c, d, st));
-  return hipGetLastError();
+  MSC_K_SWITCH(c.K, return launch_demand_k<K>(c, d, st), return launch_demand_w1(c, d, st),
+               return launch_demand_w2(c, d, st));
+  return hipSuccess;
 }
 
 hipError_t MSC_EK_FN(launch_demand_ea)(const EnvConst& c, const DevEnv* d, const EaLaunch& ea, hipStream_t st) {
   if (ea.nslots < 1) return hipSuccess;
-  MSC_K_SWITCH(c.K, launch_demand_k<K>(c, d, st, &ea), return launch_demand_ea_w1(c, d, ea, st),
+  MSC_K_SWITCH(c.K, return launch_demand_k<K>(c, d, st, &ea), return launch_demand_ea_w1(c, d, ea, st),
                return launch_demand_ea_w2(c, d, ea, st));
-  return hipGetLastError();
+  return hipSuccess;
 }
 
 #ifndef MSC_EK_WIDE
@@ -1973,7 +1973,10 @@ hipError_t launch_ea_materialize(const EnvConst& c, const DevEnv* d, int slot, i
 
 template <int K>
 static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO& io, bool gen, hipStream_t st) {
-  if (gen && c.demand_type == MSC_DEMAND_POISSON) launch_demand_k<K>(c, d, st);
+  if (gen && c.demand_type == MSC_DEMAND_POISSON) {  // the orders the step kernels below consume
+    const hipError_t ed = launch_demand_k<K>(c, d, st);
+    if (ed != hipSuccess) return ed;
+  }
   using KFn = void (*)(const DevEnv*, StepIO);
   // three phase kernels, group-per-env allocation
   const int GW = c.W <= 2 ? 2 : c.W <= 4 ? 4 : c.W <= 8 ? 8 : c.W <= 16 ? 16 : 32;

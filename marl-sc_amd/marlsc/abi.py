@@ -12,6 +12,7 @@ from pathlib import Path
 
 ABI_VERSION = 2
 MAX_W, MAX_K, MAX_R, HISTORY = 32, 16, 4096, 5
+ORDER_CAP_MAX = 1 << 24  # include/marlsc.h MSC_ORDER_CAP_MAX
 
 DEMAND = {"poisson": 0, "empirical": 1}
 ACTION = {"direct": 0, "demand_centered": 1, "base_stock": 2}
@@ -114,6 +115,8 @@ def lib() -> C.CDLL:
                                       C.POINTER(C.c_int64)]
     L.msc_env_read_timing_ea.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int32),
                                          C.POINTER(C.c_int32), C.POINTER(C.c_double)]
+    L.msc_env_work_counters.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                        C.POINTER(C.c_int64)]
     L.msc_env_read_state.argtypes = [vp, vp, vp, vp, vp]
     L.msc_env_state_bytes.argtypes = [vp]
     L.msc_env_state_bytes.restype = C.c_int64
@@ -156,7 +159,7 @@ def check(rc: int) -> None:
 
 
 EXPORTED_SYMBOLS = [
-    "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_ea_memory", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_episode_ahead", "msc_env_set_timing", "msc_env_read_timing", "msc_env_read_timing_ea", "msc_env_obs_flat",
+    "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_ea_memory", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_episode_ahead", "msc_env_set_timing", "msc_env_read_timing", "msc_env_read_timing_ea", "msc_env_work_counters", "msc_env_obs_flat",
     "msc_env_read_state", "msc_env_state_bytes", "msc_env_save_state", "msc_env_load_state", "msc_env_check",
     "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_w3_layout", "msc_mlp3_relu_forward", "msc_mlp2_relu_forward",
     "msc_mlp3_relu_forward_sampled", "msc_mlp2_relu_forward_sampled",

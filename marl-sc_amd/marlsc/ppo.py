@@ -39,6 +39,7 @@ from __future__ import annotations
 import json
 import math
 import os
+import warnings
 from collections import deque
 from dataclasses import asdict, dataclass, field
 from pathlib import Path
@@ -694,8 +695,15 @@ class PPOTrainer:
         self.env.load_state(bytes(rt["env_state"].numpy().tobytes()))
         self.env.obs.copy_(rt["obs"].to(self.device))
         self.env._t_sync = int(rt["t_sync"])
-        if "noise_step" in rt:  # (round <= 3 checkpoints held a per-rank torch generator instead)
+        if "noise_step" in rt:
             self.collector.noise_step = int(rt["noise_step"])
+        else:
+            # round <= 3 checkpoints held a per-rank torch generator instead: every collect draws T
+            # rollout steps of keyed noise, so the stream position is iterations x T (the resumed run
+            # continues the keyed stream instead of replaying the steps already taken)
+            self.collector.noise_step = self.iteration * self.collector.T
+            warnings.warn(f"{p}: checkpoint without 'noise_step' (round <= 3); keyed action noise resumes at "
+                          f"step {self.collector.noise_step} = iteration x T")
         self.learner.gen.set_state(rt["learner_gen"])
         self._ep_ret.copy_(rt["ep_ret"].to(self.device))
         self._completed = deque((float(x) for x in rt["completed"]), maxlen=self._completed.maxlen)

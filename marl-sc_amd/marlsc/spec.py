@@ -249,6 +249,10 @@ class EnvSpec:
             if np.any(self.lambda_orders >= 1e6) or np.any(self.lambda_quantity >= 20000):
                 raise ValueError("Poisson rates out of range: lambda_orders < 1e6, lambda_quantity < 20000 "
                                  "(quantities are 16-bit record fields)")
+            lam = float(self.lambda_orders.sum())
+            if np.ceil(lam + 12.0 * np.sqrt(lam + 1.0) + 64.0) > abi.ORDER_CAP_MAX:
+                raise ValueError(f"sum of lambda_orders {lam:g}: per-step order capacity exceeds "
+                                 f"{abi.ORDER_CAP_MAX} records per env (int32 record indexing)")
         if self.obs_mean is not None and self.obs_mean.shape != (self.n_features,):
             raise ValueError(f"obs_stats must have shape ({self.n_features},), got {self.obs_mean.shape}")
         if self.demand_type == "empirical" and self.trace["n_rows"] < self.episode_length:

@@ -195,6 +195,13 @@ class VecInventoryEnv:
         return {"ea_ms": ms.value, "n_ea": n.value, "slots": slots.value, "active": bool(act.value),
                 "ea_env_steps_per_launch": work.value}
 
+    def work_counters(self) -> Dict[str, float]:
+        """Demand work issued since create (msc_env_work_counters): episode-ahead generation launches
+        and their env-steps, per-step demand launches, step calls."""
+        la, ew, dl, st = C.c_int64(), C.c_double(), C.c_int64(), C.c_int64()
+        abi.check(abi.lib().msc_env_work_counters(self._h, C.byref(la), C.byref(ew), C.byref(dl), C.byref(st)))
+        return {"ea_launches": la.value, "ea_env_steps": ew.value, "demand_launches": dl.value, "steps": st.value}
+
     def alloc_info(self) -> Dict[str, torch.Tensor]:
         """Device buffers for msc_step_info (the reference's collect_step_info dict)."""
         E, W, K, R = self.n_envs, self.W, self.K, self.R

@@ -190,6 +190,34 @@ def test_sharding_invariance():
         assert torch.equal(of, torch.cat([ol, oh]))
 
 
+@pytest.mark.parametrize("n_ranks", [2, 4, 8])
+def test_strong_sharding_matches_one_rank_32768(n_ranks):
+    # BASELINE configs[3]: 32,768 envs in total, rank g of N owning global env ids
+    # [g * E / N, (g + 1) * E / N) (bench.py --scaling strong). Each shard steps the same trajectories
+    # as the one-rank handle over all 32,768 envs although the library picks other kernels per shard
+    # size (lane allocator + per-step demand at >= 16,384 envs; scan allocator + episode-ahead demand
+    # at <= 8,192), across two episode boundaries
+    E = 32768
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=15)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    full = _vec(spec, E, base_seed=77)
+    n = E // n_ranks
+    shards = [_vec(spec, n, base_seed=77, env_index_offset=g * n) for g in range(n_ranks)]
+    of = full.reset().clone()
+    for g, sh in enumerate(shards):
+        assert torch.equal(sh.reset(), of[g * n:(g + 1) * n])
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    for _ in range(40):
+        act = torch.rand((E, 8, 5), generator=gen, device="cuda") * 2 - 1
+        o, r = (x.clone() for x in full.step(act)[:2])
+        for g, sh in enumerate(shards):
+            os_, rs = sh.step(act[g * n:(g + 1) * n].contiguous())[:2]
+            assert torch.equal(os_, o[g * n:(g + 1) * n]) and torch.equal(rs, r[g * n:(g + 1) * n])
+    for x in [full] + shards:
+        x.check()
+        x.close()
+
+
 def test_save_load_state_roundtrip():
     d, meta = load("variant_b")
     env = _vec(spec_of(d, meta), 64, base_seed=3)

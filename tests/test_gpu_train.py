@@ -111,6 +111,28 @@ def test_experiment_cli_single_then_evaluate(tmp_path):
     assert res["eval/episodes"] == 3 and res["iteration"] == 2
 
 
+def test_run_experiment_script_drives_training_and_evaluation(tmp_path):
+    # the entry the north star names: `bash scripts/run_experiment.sh` (the reference's
+    # scripts/run_experiment.sh:52-68 -- `--mode single` then `--mode evaluate` with the same storage
+    # dir / experiment name / root seed) on BASELINE configs[0] (2 warehouses x 4 regions x 2 SKUs,
+    # the reference's IPPO config), shortened through EXTRA_ARGS
+    import os
+    import subprocess
+    env = dict(os.environ, ENV_CONFIG="./config_files/environments/env_c1_2wh4r2sku.yaml",
+               ALGO_CONFIG="./config_files/algorithms/ippo.yaml", STORAGE_DIR=str(tmp_path), EXPERIMENT_NAME="SH",
+               ROOT_SEED="42", EVAL_EPISODES="2", NGPUS="1",
+               EXTRA_ARGS="--num-iterations 2 --envs 16 --rollout-len 4")
+    r = subprocess.run(["bash", str(REPO / "scripts" / "run_experiment.sh")], env=env, cwd=str(tmp_path),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = tmp_path / "SH"
+    lines = (out / "training_metrics.jsonl").read_text().strip().splitlines()
+    assert len(lines) == 2 and json.loads(lines[-1])["training_iteration"] == 2
+    assert (out / "checkpoint_final" / "learner_state.pt").exists() and (out / "module_weights.pt").exists()
+    res = json.loads((out / "eval_results.json").read_text())
+    assert res["eval/episodes"] == 2 and res["iteration"] == 2
+
+
 def test_experiment_resume_truncates_metrics_and_exports_module_weights(tmp_path):
     # the reference runner's run directory (runner.py:163-395): checkpoint_<N> every checkpoint_freq
     # iterations, checkpoint_best on a new best train return, checkpoint_final, module_weights.pt

@@ -140,6 +140,12 @@ def test_shape_caps_agree_across_header_abi_spec():
     for W, K in ((33, 4), (4, 17)):
         with pytest.raises(ValueError):
             EnvSpec.from_config(make_synthetic_env_config(W, 6, K), {"include_warehouse_id": True})
+    # per-step order capacity (int32 record indexing, capi.hip): the header's cap = the mirror's, and a
+    # configuration past it (rates just under the 1e6 bound in 4,096 regions) is rejected by the spec
+    assert int(eval(re.search(r"#define MSC_ORDER_CAP_MAX \(([^)]*)\)", hdr).group(1))) == abi.ORDER_CAP_MAX
+    EnvSpec.from_config(make_synthetic_env_config(2, 4096, 1, lambda_orders=4000.0), {"include_warehouse_id": True})
+    with pytest.raises(ValueError, match="order capacity"):
+        EnvSpec.from_config(make_synthetic_env_config(2, 4096, 1, lambda_orders=9.9e5), {"include_warehouse_id": True})
 
 
 def test_seed_manager_semantics():
