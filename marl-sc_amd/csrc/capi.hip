@@ -473,6 +473,22 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     if (c.alloc_impl == 1 && !al_env && W <= 8 && alloc_scan_supported(W, K)) c.alloc_impl = 2;
     if (al_env && strcmp(al_env, "scan") == 0) c.alloc_impl = alloc_scan_supported(W, K) ? 2 : 1;
     c.scan_defer = 1;
+    {
+      // step_b's block tables ({of, ov} rows [2][R][W] f64 + closest [R] i32) in LDS: when small
+      // (16 KB, room for the blocks of the pipelined demand kernel beside the step), or, with
+      // empirical demand (no demand kernel beside the step), when the step_b blocks one CU holds at
+      // this env count fit its 160 KB with them (C5, 8,192 envs x 16 warehouses: 2 blocks of 16 KB of
+      // record windows + 65 KB of tables); otherwise each region change reads its cost row from L2
+      int ncu = 256;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
+      const int gw = W <= 2 ? 2 : W <= 4 ? 4 : W <= 8 ? 8 : W <= 16 ? 16 : 32;
+      const int64_t blocks = (n_envs * gw + 255) / 256, per_cu = (blocks + ncu - 1) / ncu;
+      const size_t tab = (size_t)2 * R * W * sizeof(double) + (size_t)R * sizeof(int32_t);
+      const size_t blk = (size_t)4 * 2 * 128 * 16 + tab;  // 4 waves x 2 windows x SB_REC records + tables
+      c.sb_tab = tab <= 16 * 1024 ? 1
+               : (d->demand_type == MSC_DEMAND_EMPIRICAL && blk <= 160 * 1024 && (int64_t)blk * per_cu <= 160 * 1024) ? 1 : 0;
+      if (const char* st = getenv("MSC_SB_TAB")) c.sb_tab = atoi(st) != 0 && blk <= 160 * 1024 ? 1 : 0;
+    }
     if (const char* sd = getenv("MSC_SCAN_DEFER")) c.scan_defer = atoi(sd) != 0 ? 1 : 0;
     // episode-ahead Poisson demand when the envs are too few to fill the chip with per-step demand
     // chains (MSC_EA=0|1 forces it off / on)

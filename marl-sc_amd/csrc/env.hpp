@@ -47,6 +47,7 @@ struct EnvConst {
   int32_t ea_S;         // episode-ahead demand: episode slots per env (0: off)
   int32_t scan_defer;   // alloc_scan_kernel: lost-sales shares deferred to a post-pass (MSC_SCAN_DEFER=0: inline)
   int32_t demand_ptrs;  // 1: some Poisson rate >= 10 (numpy's PTRS branch): the sequential sampler demand_seq_kernel
+  int32_t sb_tab;       // 1: step_b_kernel stages the {of, ov} rows and closest warehouses in LDS (its TAB form)
   uint32_t flags;
   int64_t E;
   int64_t ea_cap;       // episode-ahead demand: order records per (slot, env) episode

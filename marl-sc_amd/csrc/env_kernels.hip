@@ -1270,7 +1270,6 @@ __host__ __device__ constexpr int step_b_chunk(int GW, int NV) { return SB_REC /
 __host__ __device__ constexpr size_t step_b_tab_bytes(int R, int W) {
   return (size_t)2 * R * W * sizeof(double) + (size_t)R * sizeof(int32_t);
 }
-constexpr size_t STEP_B_TAB_MAX = 16 * 1024;
 __host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab) {
   return (size_t)4 * 2 * SB_REC * 16 + (tab ? step_b_tab_bytes(R, W) : 0);
 }
@@ -1287,6 +1286,15 @@ __host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab) {
 #endif
 #ifndef MSC_SB_WPE
 #define MSC_SB_WPE 5
+#endif
+// 16- and 32-lane groups (9-32 warehouses): 4 envs per wave or fewer, so 8,192 envs (C5) are 2,048
+// waves, 2 per SIMD: a 96-VGPR budget only spilled the order loop to scratch (whose reloads wait on
+// vmcnt, i.e. also for the record window's LDS-DMA in flight); 128 VGPRs hold it
+#ifndef MSC_SB_WPE16
+#define MSC_SB_WPE16 4
+#endif
+#ifndef MSC_SB_F32KEY
+#define MSC_SB_F32KEY 1  // step_b argmin over f32-rounded cost keys (64-bit only on an f32 tie)
 #endif
 #ifndef MSC_SB_BPERM
 #define MSC_SB_BPERM 0  // 1: winner's fill broadcast by ds_bpermute (A/B, lost at C5: 0.908 vs 0.903 ms/step)
@@ -1339,7 +1347,7 @@ __global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restri
 
 // (above 8 SKUs the K-wide register arrays of a lane need the larger budget of 2 waves per SIMD)
 template <int K, int GW, bool DBG, bool TAB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : GW >= 16 ? MSC_SB_WPE16 : MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int W = c.W, WK = W * K, R = c.R;
@@ -1514,29 +1522,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
   PROF_DECL(q_iter);
   PROF_DECL(q_nfin);
   PROF_T(q_t0);
+  // Software pipeline over the orders: record oi + 1 is read from its window while order oi is
+  // allocated, and its demand weight (and, with the tables in LDS, its region's cost row) is
+  // prepared at the end of iteration oi; the window holding order oi + 1 is therefore made resident
+  // one order earlier than it is consumed. (A cost row read from global memory is not prefetched:
+  // its wait would also wait for the record window's LDS-DMA in flight, which shares vmcnt.)
+  int r_nx = -1, d_nx[K];
+  double tw_nx = 0.0, cof_nx = 0.0, cov_nx = 0.0;
+  auto fetch = [&](int q) {  // record q of this lane's env (its window is resident); -1: no order q
+    union {
+      uint4 v[NVR];
+      uint16_t h[8 * NVR];
+    } ur;
+#pragma unroll
+    for (int j = 0; j < NVR; j++) ur.v[j] = win[((q / CH) & 1) * SB_REC + ((q % CH) * NVR + j) * EPW + myjj];
+    r_nx = q < n_orders ? (int)ur.h[0] : -1;
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) d_nx[sk] = ur.h[1 + sk];
+  };
+  auto prep = [&](int r_prev) {  // order.sku_demands . sku_weights of the fetched order; its cost row
+    double t = 0.0;
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) t += (double)d_nx[sk] * skw[sk];
+    tw_nx = t;
+    if constexpr (TAB) {
+      if (r_nx >= 0 && r_nx != r_prev && wl) {
+        cof_nx = cost_of(r_nx);
+        cov_nx = cost_ov(r_nx);
+      } else {
+        cof_nx = cof;
+        cov_nx = cov;
+      }
+    }
+  };
+  fetch(0);
+  prep(-1);
   for (int oi = 0; oi <= wmax; oi++) {
-    if (oi > 0 && oi % CH == 0) {  // wave-uniform: window oi / CH is due, start the one after
-      if (oi + CH <= wmax) {
-        issue(oi / CH + 1);
+    // wave-uniform: the window holding order oi + 1 is due, start the one after. (Record oi, the
+    // last one of the buffer the new LDS-DMA overwrites, was read in the previous iteration.)
+    const int q = oi + 1;
+    if (q % CH == 0 && q <= wmax) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (q + CH <= wmax) {
+        issue(q / CH + 1);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPL) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
     if (oi > n_orders) continue;  // this env is done (lanes of busier envs go on)
-    int r = -1;
+    const int r = r_nx;
     int d[K];
-    {
-      union {
-        uint4 v[NVR];
-        uint16_t h[8 * NVR];
-      } ur;
 #pragma unroll
-      for (int j = 0; j < NVR; j++) ur.v[j] = win[((oi / CH) & 1) * SB_REC + ((oi % CH) * NVR + j) * EPW + myjj];
-      if (oi < n_orders) r = ur.h[0];
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
-    }
+    for (int sk = 0; sk < K; sk++) d[sk] = d_nx[sk];
+    const double tw = tw_nx;  // order.sku_demands.dot(sku_weights) (demand_allocator.py:168-170)
+    const double cof_r = cof_nx, cov_r = cov_nx;
+    if (q < n_orders) fetch(q);  // the next record's LDS read in flight during this order
+    else r_nx = -1;
     // (prof build: the time of this block and its passes counted for the whole wave, i.e. also when
     // only another env of the wave changes region)
     PROF_T(q_f0);
@@ -1546,8 +1588,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     if (r != cur) {
       if (cur >= 0) finalize(cur);
       if (r >= 0 && wl) {
-        cof = cost_of(r);
-        cov = cost_ov(r);
+        if constexpr (TAB) {
+          cof = cof_r;
+          cov = cov_r;
+        } else {
+          cof = cost_of(r);
+          cov = cost_ov(r);
+        }
       }
       cur = r;
       lost_cnt = 0;
@@ -1557,14 +1604,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     PROF_ADD(q_fin, PROF_NOW() - q_f0);
     if (oi == n_orders) continue;
     bool any_d = false;
-    double tw = 0.0;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       dsum[sk] += d[sk];
       any_d |= d[sk] > 0;
-      tw += (double)d[sk] * skw[sk];
     }
-    if (!any_d) continue;  // an empty order ships nothing and is never lost
+    if (!any_d) {  // an empty order ships nothing and is never lost
+      if (q < n_orders) prep(r);
+      continue;
+    }
     int rem[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
@@ -1572,6 +1620,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     // total-order key of the cost (negatives and -0.0 included), so the group min is an integer min
     const uint64_t cbits = (uint64_t)__double_as_longlong(mycost + 0.0);
     const uint64_t ckey = cbits ^ ((uint64_t)((int64_t)cbits >> 63) | 0x8000000000000000ull);
+#if MSC_SB_F32KEY
+    // and of its f32 rounding: f64 -> f32 is monotone, so the cheapest warehouse is among the lanes
+    // at the minimum f32 key; the 64-bit minimum runs only when two of them share that key
+    const uint32_t fbits = __float_as_uint((float)mycost + 0.0f);
+    const uint32_t fkey = fbits ^ ((uint32_t)((int32_t)fbits >> 31) | 0x80000000u);
+#endif
     int used = 0;
     bool open = true;
     PROF_T(q_a0);
@@ -1582,24 +1636,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       bool has = false;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) has |= rem[sk] > 0 && inv[sk] > 0;
-      const uint64_t key = (has && wl) ? ckey : ~0ull;
-      uint64_t mk = key;
+      int bw;
+#if MSC_SB_F32KEY
+      const uint32_t k32 = (has && wl) ? fkey : 0xFFFFFFFFu;
+      const uint32_t m32 =
+          (uint32_t)group_reduce<GW>((int)k32, [](int x, int y) { return (uint32_t)y < (uint32_t)x ? y : x; });
+      if (m32 == 0xFFFFFFFFu) break;  // nobody holds a still-needed SKU (finite costs: keys < 0xFF800001)
+      const uint32_t tg = (uint32_t)(__ballot(k32 == m32) >> gbase) & (uint32_t)((1ull << GW) - 1ull);
+      if (__ballot(__builtin_popcount(tg) > 1) == 0ull) {
+        bw = __builtin_ctz(tg);
+      } else
+#endif
       {
-        auto step = [&](uint64_t o) { mk = o < mk ? o : mk; };
-        auto dpp64 = [](auto f, uint64_t v) {
-          const int lo = f((int)(unsigned)v), hi = f((int)(unsigned)(v >> 32));
-          return ((uint64_t)(unsigned)hi << 32) | (unsigned)lo;
-        };
-        step(dpp64([](int v) { return dpp_x<0>(v); }, mk));
-        if constexpr (GW >= 4) step(dpp64([](int v) { return dpp_x<1>(v); }, mk));
-        if constexpr (GW >= 8) step(dpp64([](int v) { return dpp_x<2>(v); }, mk));
-        if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
-        if constexpr (GW >= 32) step(dpp64([](int v) { return dpp_x<4>(v); }, mk));
+#if MSC_SB_F32KEY
+        const uint64_t key = (has && wl && k32 == m32) ? ckey : ~0ull;
+#else
+        const uint64_t key = (has && wl) ? ckey : ~0ull;
+#endif
+        uint64_t mk = key;
+        {
+          auto step = [&](uint64_t o) { mk = o < mk ? o : mk; };
+          auto dpp64 = [](auto f, uint64_t v) {
+            const int lo = f((int)(unsigned)v), hi = f((int)(unsigned)(v >> 32));
+            return ((uint64_t)(unsigned)hi << 32) | (unsigned)lo;
+          };
+          step(dpp64([](int v) { return dpp_x<0>(v); }, mk));
+          if constexpr (GW >= 4) step(dpp64([](int v) { return dpp_x<1>(v); }, mk));
+          if constexpr (GW >= 8) step(dpp64([](int v) { return dpp_x<2>(v); }, mk));
+          if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
+          if constexpr (GW >= 32) step(dpp64([](int v) { return dpp_x<4>(v); }, mk));
+        }
+#if !MSC_SB_F32KEY
+        if (mk == ~0ull) break;  // nobody holds a still-needed SKU
+#endif
+        // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
+        const uint64_t tie = __ballot(key == mk);
+        bw = __builtin_ctzll(tie >> gbase);
       }
-      if (mk == ~0ull) break;  // nobody holds a still-needed SKU
-      // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
-      const uint64_t tie = __ballot(key == mk);
-      const int bw = __builtin_ctzll(tie >> gbase);
       const bool me = w == bw;
       int fl[K];
 #pragma unroll
@@ -1660,6 +1733,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       u[sk] += rem[sk] > 0 ? rem[sk] : 0;
     }
     lost_cnt += anyrem ? 1 : 0;
+    if (q < n_orders) prep(r);
   }
   PROF_ADD(q_all, PROF_NOW() - q_t0);
   PROF_FLUSH(10, q_all);
@@ -2000,7 +2074,7 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     cc = (c.W <= 8 && c.obs_ring_reg) ? (dbg ? (KFn)step_c_kernel<K, true, 8> : (KFn)step_c_kernel<K, false, 8>)
                                       : (dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>);
   }
-  const bool tab = step_b_tab_bytes(c.R, c.W) <= STEP_B_TAB_MAX;
+  const bool tab = c.sb_tab != 0;  // (capi.hip: small tables, or room at this occupancy)
   KFn b;
 #define MSC_SB(GWV)                                                                                   \
   (dbg ? (tab ? (KFn)step_b_kernel<K, GWV, true, true> : (KFn)step_b_kernel<K, GWV, true, false>)   \
@@ -2016,7 +2090,12 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     if (ea != hipSuccess) return ea;
   } else {
     if (c.alloc_sort) launch_alloc_sort(d, io, st);
-    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), step_b_lds_bytes(c.R, c.W, tab), st, d, io);
+    const size_t lds_b = step_b_lds_bytes(c.R, c.W, tab);
+    if (lds_b > 64 * 1024) {
+      const hipError_t e = hipFuncSetAttribute((const void*)b, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), lds_b, st, d, io);
   }
   const int stage_w = c.obs_stage ? (c.W + (c.obs_stage > 1 ? c.obs_stage : 1) - 1) / (c.obs_stage > 1 ? c.obs_stage : 1) : 0;
   const size_t lds_c = (size_t)c.W * BS * sizeof(double) +
