@@ -178,7 +178,10 @@ def window_work(w0: dict, w1: dict, n_envs: int, steps: int) -> dict:
     dl = int(w1["demand_launches"] - w0["demand_launches"])
     return {"ea_launches_in_window": ea_l, "ea_env_steps_in_window": ea_w, "demand_launches_in_window": dl,
             "demand_env_steps_in_window": ea_w + dl * n_envs, "env_steps_timed": int(n_envs) * int(steps),
-            "steps_in_window": int(w1["steps"] - w0["steps"])}
+            "steps_in_window": int(w1["steps"] - w0["steps"]),
+            # steps of demand per env generated beyond (> 0) or drawn from the buffer built before the
+            # window (< 0): a window is sustained when this is not far below zero
+            "ahead_change_steps": round((ea_w + dl * n_envs - int(n_envs) * int(steps)) / max(1, n_envs), 1)}
 
 
 def time_rollout(envs, module, T: int, world: int, seed: int, warm: int = 1, reps: int = 1, with_window: bool = False):
@@ -238,18 +241,23 @@ def c2_line(args, rank: int):
     # episodes are generated in two bulk launches that keep the generation stream busy for the first
     # ~20 episodes (a 12-episode window after 12 read 162 M where 48 episodes read 175.5 M,
     # profiles/r03/ab_ea_slots.txt)
+    # round 5: 96 episodes after 96 (24 refill periods each): the 24-after-24 window of round 4 held
+    # generation launches for only 75 % of the env-steps it timed, a 48-episode window 92 % (one refill
+    # of 4 slots x 100 steps short: a refill in flight at the window's start was launched before it);
+    # the line's `window` object reports what was generated inside the window, and `value_sustained`
+    # scales `value` by min(1, generated / timed) as a lower bound
     period = 4 * T
-    steps = max(6 * period, -(-args.steps // period) * period)
-    warm = 6 * period
+    steps = max(args.c2_episodes * T, -(-args.steps // period) * period)
+    warm = args.c2_episodes * T
     dt, tm = time_env(env, pool, steps, warm, 1, ea=True)
     rc = RolloutConfig.from_algorithm_config(algo)
     torch.manual_seed(0)
     module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
-    # four refill periods (16 episodes = 16 rollouts) timed after one: rollouts run 0.21 ms per step
-    # while no generation launch is in flight and ~0.34 while one is (the launches of one refill take
-    # most of the next 4 rollouts), so a window of one or two periods read 0.21-0.29 ms per step
-    # depending on its phase (profiles/r04/c2_rollout_phases.txt); 16 rollouts average the phases
-    t_roll, roll_win = time_rollout(env, module, T, 1, seed=rank, warm=4, reps=16, with_window=True) if args.rollout_T > 0 else (0.0, None)
+    # eight refill periods (32 episodes = 32 rollouts) timed after two: a generation launch of one
+    # refill runs beside the next few rollouts, so a window of one or two periods read 0.21-0.29 ms per
+    # step depending on its phase (profiles/r04/c2_rollout_phases.txt); 16 rollouts still held
+    # generation for only 62 % of their env-steps (round 5), hence the longer window
+    t_roll, roll_win = time_rollout(env, module, T, 1, seed=rank, warm=8, reps=32, with_window=True) if args.rollout_T > 0 else (0.0, None)
     a_h, c_h = rc.actor["hidden_sizes"], rc.critic["hidden_sizes"]
     out = {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x {spec.K} SKUs "
                        f"(BASELINE configs[1])",
@@ -261,7 +269,9 @@ def c2_line(args, rank: int):
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4),
                           "demand_ea_chunk": round(tm["ea_ms"], 4) if tm["n_ea"] else None,
                           "demand_per_step": round(tm["demand_ms"], 4) if tm["n_demand"] else None},
-           "window": tm["window"]}
+           "window": tm["window"],
+           "value_sustained": round(E * spec.W * steps / dt * min(1.0, tm["window"]["demand_env_steps_in_window"]
+                                                                   / max(1, tm["window"]["env_steps_timed"])), 1)}
     # the step kernels against the VALU issue peak: PMC instruction counts of the same workload
     # (scripts/gpu_profile.sh -> profiles/traffic.json) over the live step-kernel time
     tj = Path(args.traffic_json)
@@ -288,7 +298,9 @@ def c2_line(args, rank: int):
                                     f"{'-'.join(map(str, c_h))}-1 on local obs, fp32, parameter sharing",
                           "includes": "env step, actor + critic forward, Gaussian sampling, buffer writes, truncation "
                                       "bootstrap, GAE kernel, adv-norm statistics + normalise",
-                          "window": roll_win}
+                          "window": roll_win,
+                          "value_sustained": round(E * spec.W * T / t_roll * min(1.0, roll_win["demand_env_steps_in_window"]
+                                                                                  / max(1, roll_win["env_steps_timed"])), 1)}
     env.close()
     return out
 
@@ -454,6 +466,9 @@ def main():
     ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "traffic.json"))
     ap.add_argument("--rollout-T", type=int, default=100,
                     help="steps of the MAPPO rollout line (0 = skip): env + actor/critic forward + buffers + GAE")
+    ap.add_argument("--rollout-warm", type=int, default=1, help="untimed rollouts before the timed ones (MAPPO line)")
+    ap.add_argument("--rollout-reps", type=int, default=1, help="timed rollouts of the MAPPO line")
+    ap.add_argument("--c2-episodes", type=int, default=96, help="episodes of warm-up and of the timed window of the c2 line")
     ap.add_argument("--c2-envs", type=int, default=4096, help="envs of the configs[1] line (0 = skip it)")
     ap.add_argument("--c5-envs", type=int, default=8192, help="envs of the configs[4] line (0 = skip it)")
     ap.add_argument("--no-ea-line", dest="ea_line", action="store_false",
@@ -580,7 +595,8 @@ def main():
             for x in renv:
                 x.set_pipelining(os.environ.get("MSC_ROLLOUT_PIPELINE", "1") != "0")
                 x.reset()
-        t_roll, roll_win = time_rollout(renv, module, args.rollout_T, world, seed=0, with_window=True)
+        t_roll, roll_win = time_rollout(renv, module, args.rollout_T, world, seed=0, warm=args.rollout_warm,
+                                        reps=args.rollout_reps, with_window=True)
     # (4) the HBM-bound kernel of the rollout: msc_gae (GAE reverse scan + advantage statistics) over
     #     one MAPPO rollout's [T, E * W] sequences, timed alone with events on its stream
     gae_line = None

@@ -55,6 +55,12 @@ __device__ unsigned long long g_prof_scan[8];
 #endif
 
 constexpr int SC_WAVES = 4;  // envs (waves) per block
+// waves per SIMD the <= 8-warehouse instantiations are register-budgeted for: 4 (<= 128 VGPRs). At
+// 142 / 136 VGPRs (rounds 3-4) only 3 fit, so of configs[1]'s 4,096 one-env waves 3,072 ran and the
+// last 1,024 started as they retired: the launch took two wave lifetimes (75 us each, 142 us)
+#ifndef MSC_SC_WPE
+#define MSC_SC_WPE 4
+#endif
 constexpr int SC_WIN = 64;   // orders ranked per window (one per lane)
 #ifndef MSC_SC_PRIO
 #define MSC_SC_PRIO 3  // s_setprio: the step chain is the critical path next to the demand generator
@@ -197,7 +203,7 @@ __device__ __forceinline__ T sc_readlane(T v, int l) {
 // NS = 2 (16 warehouses, 5-6 SKUs): every per-(SKU, warehouse) quantity is a two-slot array; one
 // ranking, one permute address and one contribution mask serve both slots.
 template <int K, int GW, bool TAB>
-__global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(GW > 8 ? 3 : 1))) void alloc_scan_kernel(
+__global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(GW > 8 ? 3 : MSC_SC_WPE))) void alloc_scan_kernel(
     const DevEnv* __restrict__ dp, StepIO io) {
   constexpr int SPW = 64 / GW;        // SKU groups per wave
   constexpr int NS = sc_ns(K, GW);    // SKU slots per lane

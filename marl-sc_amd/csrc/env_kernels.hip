@@ -1293,9 +1293,6 @@ __host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab) {
 #ifndef MSC_SB_WPE16
 #define MSC_SB_WPE16 4
 #endif
-#ifndef MSC_SB_F32KEY
-#define MSC_SB_F32KEY 1  // step_b argmin over f32-rounded cost keys (64-bit only on an f32 tie)
-#endif
 #ifndef MSC_SB_BPERM
 #define MSC_SB_BPERM 0  // 1: winner's fill broadcast by ds_bpermute (A/B, lost at C5: 0.908 vs 0.903 ms/step)
 #endif
@@ -1522,63 +1519,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
   PROF_DECL(q_iter);
   PROF_DECL(q_nfin);
   PROF_T(q_t0);
-  // Software pipeline over the orders: record oi + 1 is read from its window while order oi is
-  // allocated, and its demand weight (and, with the tables in LDS, its region's cost row) is
-  // prepared at the end of iteration oi; the window holding order oi + 1 is therefore made resident
-  // one order earlier than it is consumed. (A cost row read from global memory is not prefetched:
-  // its wait would also wait for the record window's LDS-DMA in flight, which shares vmcnt.)
-  int r_nx = -1, d_nx[K];
-  double tw_nx = 0.0, cof_nx = 0.0, cov_nx = 0.0;
-  auto fetch = [&](int q) {  // record q of this lane's env (its window is resident); -1: no order q
-    union {
-      uint4 v[NVR];
-      uint16_t h[8 * NVR];
-    } ur;
-#pragma unroll
-    for (int j = 0; j < NVR; j++) ur.v[j] = win[((q / CH) & 1) * SB_REC + ((q % CH) * NVR + j) * EPW + myjj];
-    r_nx = q < n_orders ? (int)ur.h[0] : -1;
-#pragma unroll
-    for (int sk = 0; sk < K; sk++) d_nx[sk] = ur.h[1 + sk];
-  };
-  auto prep = [&](int r_prev) {  // order.sku_demands . sku_weights of the fetched order; its cost row
-    double t = 0.0;
-#pragma unroll
-    for (int sk = 0; sk < K; sk++) t += (double)d_nx[sk] * skw[sk];
-    tw_nx = t;
-    if constexpr (TAB) {
-      if (r_nx >= 0 && r_nx != r_prev && wl) {
-        cof_nx = cost_of(r_nx);
-        cov_nx = cost_ov(r_nx);
-      } else {
-        cof_nx = cof;
-        cov_nx = cov;
-      }
-    }
-  };
-  fetch(0);
-  prep(-1);
   for (int oi = 0; oi <= wmax; oi++) {
-    // wave-uniform: the window holding order oi + 1 is due, start the one after. (Record oi, the
-    // last one of the buffer the new LDS-DMA overwrites, was read in the previous iteration.)
-    const int q = oi + 1;
-    if (q % CH == 0 && q <= wmax) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (q + CH <= wmax) {
-        issue(q / CH + 1);
+    if (oi > 0 && oi % CH == 0) {  // wave-uniform: window oi / CH is due, start the one after
+      if (oi + CH <= wmax) {
+        issue(oi / CH + 1);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPL) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
     if (oi > n_orders) continue;  // this env is done (lanes of busier envs go on)
-    const int r = r_nx;
+    int r = -1;
     int d[K];
+    {
+      union {
+        uint4 v[NVR];
+        uint16_t h[8 * NVR];
+      } ur;
 #pragma unroll
-    for (int sk = 0; sk < K; sk++) d[sk] = d_nx[sk];
-    const double tw = tw_nx;  // order.sku_demands.dot(sku_weights) (demand_allocator.py:168-170)
-    const double cof_r = cof_nx, cov_r = cov_nx;
-    if (q < n_orders) fetch(q);  // the next record's LDS read in flight during this order
-    else r_nx = -1;
+      for (int j = 0; j < NVR; j++) ur.v[j] = win[((oi / CH) & 1) * SB_REC + ((oi % CH) * NVR + j) * EPW + myjj];
+      if (oi < n_orders) r = ur.h[0];
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
+    }
     // (prof build: the time of this block and its passes counted for the whole wave, i.e. also when
     // only another env of the wave changes region)
     PROF_T(q_f0);
@@ -1588,13 +1551,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     if (r != cur) {
       if (cur >= 0) finalize(cur);
       if (r >= 0 && wl) {
-        if constexpr (TAB) {
-          cof = cof_r;
-          cov = cov_r;
-        } else {
-          cof = cost_of(r);
-          cov = cost_ov(r);
-        }
+        cof = cost_of(r);
+        cov = cost_ov(r);
       }
       cur = r;
       lost_cnt = 0;
@@ -1604,15 +1562,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     PROF_ADD(q_fin, PROF_NOW() - q_f0);
     if (oi == n_orders) continue;
     bool any_d = false;
+    double tw = 0.0;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       dsum[sk] += d[sk];
       any_d |= d[sk] > 0;
+      tw += (double)d[sk] * skw[sk];
     }
-    if (!any_d) {  // an empty order ships nothing and is never lost
-      if (q < n_orders) prep(r);
-      continue;
-    }
+    if (!any_d) continue;  // an empty order ships nothing and is never lost
     int rem[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
@@ -1620,12 +1577,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     // total-order key of the cost (negatives and -0.0 included), so the group min is an integer min
     const uint64_t cbits = (uint64_t)__double_as_longlong(mycost + 0.0);
     const uint64_t ckey = cbits ^ ((uint64_t)((int64_t)cbits >> 63) | 0x8000000000000000ull);
-#if MSC_SB_F32KEY
-    // and of its f32 rounding: f64 -> f32 is monotone, so the cheapest warehouse is among the lanes
-    // at the minimum f32 key; the 64-bit minimum runs only when two of them share that key
-    const uint32_t fbits = __float_as_uint((float)mycost + 0.0f);
-    const uint32_t fkey = fbits ^ ((uint32_t)((int32_t)fbits >> 31) | 0x80000000u);
-#endif
     int used = 0;
     bool open = true;
     PROF_T(q_a0);
@@ -1636,43 +1587,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       bool has = false;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) has |= rem[sk] > 0 && inv[sk] > 0;
-      int bw;
-#if MSC_SB_F32KEY
-      const uint32_t k32 = (has && wl) ? fkey : 0xFFFFFFFFu;
-      const uint32_t m32 =
-          (uint32_t)group_reduce<GW>((int)k32, [](int x, int y) { return (uint32_t)y < (uint32_t)x ? y : x; });
-      if (m32 == 0xFFFFFFFFu) break;  // nobody holds a still-needed SKU (finite costs: keys < 0xFF800001)
-      const uint32_t tg = (uint32_t)(__ballot(k32 == m32) >> gbase) & (uint32_t)((1ull << GW) - 1ull);
-      if (__ballot(__builtin_popcount(tg) > 1) == 0ull) {
-        bw = __builtin_ctz(tg);
-      } else
-#endif
+      const uint64_t key = (has && wl) ? ckey : ~0ull;
+      uint64_t mk = key;
       {
-#if MSC_SB_F32KEY
-        const uint64_t key = (has && wl && k32 == m32) ? ckey : ~0ull;
-#else
-        const uint64_t key = (has && wl) ? ckey : ~0ull;
-#endif
-        uint64_t mk = key;
-        {
-          auto step = [&](uint64_t o) { mk = o < mk ? o : mk; };
-          auto dpp64 = [](auto f, uint64_t v) {
-            const int lo = f((int)(unsigned)v), hi = f((int)(unsigned)(v >> 32));
-            return ((uint64_t)(unsigned)hi << 32) | (unsigned)lo;
-          };
-          step(dpp64([](int v) { return dpp_x<0>(v); }, mk));
-          if constexpr (GW >= 4) step(dpp64([](int v) { return dpp_x<1>(v); }, mk));
-          if constexpr (GW >= 8) step(dpp64([](int v) { return dpp_x<2>(v); }, mk));
-          if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
-          if constexpr (GW >= 32) step(dpp64([](int v) { return dpp_x<4>(v); }, mk));
-        }
-#if !MSC_SB_F32KEY
-        if (mk == ~0ull) break;  // nobody holds a still-needed SKU
-#endif
-        // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
-        const uint64_t tie = __ballot(key == mk);
-        bw = __builtin_ctzll(tie >> gbase);
+        auto step = [&](uint64_t o) { mk = o < mk ? o : mk; };
+        auto dpp64 = [](auto f, uint64_t v) {
+          const int lo = f((int)(unsigned)v), hi = f((int)(unsigned)(v >> 32));
+          return ((uint64_t)(unsigned)hi << 32) | (unsigned)lo;
+        };
+        step(dpp64([](int v) { return dpp_x<0>(v); }, mk));
+        if constexpr (GW >= 4) step(dpp64([](int v) { return dpp_x<1>(v); }, mk));
+        if constexpr (GW >= 8) step(dpp64([](int v) { return dpp_x<2>(v); }, mk));
+        if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
+        if constexpr (GW >= 32) step(dpp64([](int v) { return dpp_x<4>(v); }, mk));
       }
+      if (mk == ~0ull) break;  // nobody holds a still-needed SKU
+      // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
+      const uint64_t tie = __ballot(key == mk);
+      const int bw = __builtin_ctzll(tie >> gbase);
       const bool me = w == bw;
       int fl[K];
 #pragma unroll
@@ -1733,7 +1665,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       u[sk] += rem[sk] > 0 ? rem[sk] : 0;
     }
     lost_cnt += anyrem ? 1 : 0;
-    if (q < n_orders) prep(r);
   }
   PROF_ADD(q_all, PROF_NOW() - q_t0);
   PROF_FLUSH(10, q_all);
