@@ -34,6 +34,7 @@
 
 #include "env.hpp"
 #include "kcommon.hpp"
+#include "obs_common.hpp"
 
 namespace msc {
 
@@ -90,6 +91,14 @@ struct ScLostLds {
   int32_t lr_r[SC_LR];         // region id
   int32_t lr_cnt[SC_LR];       // lost orders
   double lr_wt[64];            // one pass's shares [i % (64 / GW)][w]
+};
+// fused phase C: the per-(SKU, warehouse) inputs of the observation builder, [field][s * GW + w]
+// (aliases the deferred-region block, flushed by then; allocated as the larger of the two)
+constexpr int SC_FC_RING = 4;  // pending-ring slots staged (lead times <= 3)
+enum : int { FC_INV, FC_DH, FC_SH, FC_SA, FC_PEND, FC_ELT, FC_FC, FC_RM, FC_RING, FC_HIST = FC_RING + SC_FC_RING,
+             FC_NF = FC_HIST + MSC_HISTORY };
+struct ScFcLds {
+  int32_t v[FC_NF][64];
 };
 constexpr size_t sc_tab_bytes(int R, int GW) { return (size_t)(R | 1) * GW * 16; }
 constexpr size_t SC_TAB_MAX = 32 * 1024;
@@ -202,12 +211,18 @@ __device__ __forceinline__ T sc_readlane(T v, int l) {
 // limiting the warehouses per order every order is its own batch, with per-order ballots.)
 // NS = 2 (16 warehouses, 5-6 SKUs): every per-(SKU, warehouse) quantity is a two-slot array; one
 // ranking, one permute address and one contribution mask serve both slots.
-template <int K, int GW, bool TAB>
+// FC: phase C fused (step_c_kernel's work for the wave's env: forecast / history, rewards, the
+// observations, the in-kernel reset at truncation; one slot per lane, rings of <= SC_FC_RING slots).
+// FA (with FC): phase A fused too (step_a_kernel: action rescale, orders into the ring, arrivals,
+// inbound cost) for fixed lead times and Poisson demand (no per-env RNG work in phase A)
+template <int K, int GW, bool TAB, bool FC = false, bool FA = false>
 __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(GW > 8 ? 3 : MSC_SC_WPE))) void alloc_scan_kernel(
     const DevEnv* __restrict__ dp, StepIO io) {
   constexpr int SPW = 64 / GW;        // SKU groups per wave
   constexpr int NS = sc_ns(K, GW);    // SKU slots per lane
   static_assert(K <= 6 && NS <= 2 && GW <= 16, "one uint4 per order record; <= 2 slots");
+  static_assert(!FC || NS == 1, "the fused phase C takes one (SKU, warehouse) slot per lane");
+  static_assert(!FA || FC, "phase A is fused only with phase C");
   using Rho = ScRho<GW>;
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
@@ -236,6 +251,10 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
   ScLostLds<GW>* Ll =
       reinterpret_cast<ScLostLds<GW>*>(reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) + wave;
   constexpr int LA = ScLostLds<GW>::LA;
+  // FA: the ring after phase A, [q][lane], after the tail blocks (their size: alloc_scan_lds_bytes)
+  constexpr size_t TAILB = sizeof(ScLostLds<GW>) > sizeof(ScFcLds) ? sizeof(ScLostLds<GW>) : sizeof(ScFcLds);
+  int32_t* Lra = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) +
+                                            SC_WAVES * TAILB) + wave * SC_FC_RING * 64;
   const int RS = R | 1;
   if constexpr (TAB) {
     for (int i = threadIdx.x; i < R * GW; i += blockDim.x) {
@@ -282,10 +301,76 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
   int64_t gi[NS];
   int inv[NS], inv0[NS], qsr[NS], u[NS], dsum[NS], inc_h[NS], shh_h[NS], fi[NS];
   double lost[NS], ovacc[NS];
+  const int t_now = FC ? __builtin_amdgcn_readfirstlane(s.t[e]) : 0;
+  // FA: phase A (step_a_kernel's per-(SKU, warehouse) work) on this lane's slot; the ring after it
+  // stays in registers for phase C; the warehouse's inbound cost reaches lane w (sg == 0)
+  double inb_a = 0.0;
+  if constexpr (FA) {
+    const int RING = c.RING, slot = t_now % RING;
+    const int i = w * K + skj[0];
+    const int64_t g = (int64_t)i * E + e;
+    double tF = 0.0, tV = 0.0;
+    int iv = 0;
+    int ring_a[SC_FC_RING] = {};
+    if (lvj[0]) {
+      const float a = io.actions[(e * W + w) * K + skj[0]];
+      const int inc_old = s.inc[g];
+      iv = s.inv[g];
+      int pend = 0;
+#pragma unroll
+      for (int q = 0; q < SC_FC_RING; q++) {
+        ring_a[q] = q < RING ? s.ring_q[((int64_t)i * RING + q) * E + e] : 0;
+        pend += ring_a[q];
+      }
+      const int qi = rescale_action(c, skj[0], a, inc_old, pend);
+      const int elt = c.elt[i];
+      if (dbg) {
+        if (info.inventory_before) info.inventory_before[e * WK + i] = iv;
+        if (info.pending_total) info.pending_total[e * WK + i] = pend;
+        if (info.order_quantities) info.order_quantities[e * WK + i] = qi;
+      }
+      // _apply_arrivals: the orders whose actual lead time equals their age (arrival == t)
+#pragma unroll
+      for (int q = 0; q < SC_FC_RING; q++) {
+        int age = (t_now - q) % RING;
+        if (age < 0) age += RING;
+        const bool arrive = q < RING && q != slot && ring_a[q] != 0 && elt == age;
+        iv += arrive ? ring_a[q] : 0;
+        if (arrive) {
+          ring_a[q] = 0;
+          s.ring_q[((int64_t)i * RING + q) * E + e] = 0;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < SC_FC_RING; q++) ring_a[q] = q == slot ? qi : ring_a[q];
+      s.ring_q[((int64_t)i * RING + slot) * E + e] = qi;  // _apply_orders: the slot of order time t
+      tF = qi > 0 ? c.inF[i] : 0.0;
+      tV = ((double)qi * c.skw[skj[0]]) * c.inV[i];
+    }
+    inv[0] = iv;
+#pragma unroll
+    for (int q = 0; q < SC_FC_RING; q++) Lra[q * 64 + lane] = ring_a[q];  // (for phase C)
+    // inbound cost (reward_calculator.py:144-151): fixed and variable terms summed over SKUs in order
+    Lw->dscr[lane] = tF;
+    wave_sync();
+    double sF = 0.0, sV = 0.0;
+    if (sg == 0 && w < W)
+#pragma unroll
+      for (int j = 0; j < K; j++) sF += Lw->dscr[j * GW + w];
+    wave_sync();
+    Lw->dscr[lane] = tV;
+    wave_sync();
+    if (sg == 0 && w < W) {
+#pragma unroll
+      for (int j = 0; j < K; j++) sV += Lw->dscr[j * GW + w];
+      inb_a = sF + sV;
+    }
+    wave_sync();
+  }
 #pragma unroll
   for (int j = 0; j < NS; j++) {
     gi[j] = (int64_t)(w * K + skj[j]) * E + e;
-    inv[j] = lvj[j] ? s.inv[gi[j]] : 0;
+    if (!FA) inv[j] = lvj[j] ? s.inv[gi[j]] : 0;
     inv0[j] = inv[j];
     qsr[j] = u[j] = dsum[j] = inc_h[j] = shh_h[j] = 0;
     lost[j] = ovacc[j] = 0.0;
@@ -679,23 +764,161 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
   for (int j = 0; j < NS; j++) {
     if (!lvj[j]) continue;
     s.inv[gi[j]] = inv[j];
-    s.sc_sht[gi[j]] = inv0[j] - inv[j];  // shipped this step = the inventory drop
-    s.sc_shh[gi[j]] = home_done ? shh_h[j] : 0;
-    if (home_done) s.inc[gi[j]] = inc_h[j];  // (step_a zeroed it: a home region without orders leaves 0)
+    if (!FC) {  // (step_c's inputs)
+      s.sc_sht[gi[j]] = inv0[j] - inv[j];  // shipped this step = the inventory drop
+      s.sc_shh[gi[j]] = home_done ? shh_h[j] : 0;
+    }
+    if (FA) s.inc[gi[j]] = home_done ? inc_h[j] : 0;  // (phase A here: nobody zeroed it)
+    else if (home_done) s.inc[gi[j]] = inc_h[j];  // (step_a zeroed it: a home region without orders leaves 0)
     if (dbg) {
       if (info.lost_sales) info.lost_sales[e * WK + w * K + skj[j]] = lost[j];
       if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + skj[j]] = inv0[j] - inv[j];
     }
   }
+  double pen_w = 0.0, out_w = 0.0;  // (lanes sg == 0, w < W)
   if (sg == 0 && w < W) {
-    double pen = 0.0, ovar = 0.0;
+    double ovar = 0.0;
 #pragma unroll
     for (int j = 0; j < K; j++) {
-      pen += Lw->dscr[j * GW + w];
+      pen_w += Lw->dscr[j * GW + w];
       ovar += Lov[j * GW + w];
     }
-    s.sc_pen[w * E + e] = pen;
-    s.sc_out[w * E + e] = ofix + ovar;
+    out_w = ofix + ovar;
+    if (!FC) {
+      s.sc_pen[w * E + e] = pen_w;
+      s.sc_out[w * E + e] = out_w;
+    }
+  }
+  if constexpr (FC) {
+    // ---- phase C (step_c_kernel, multi_env.py:307-327, 747-793; reward_calculator.py:96-190) for
+    // this wave's env, its inputs in registers: lane (s, w) holds SKU s of warehouse w after the
+    // allocation. The observation builder's per-SKU inputs are staged in LDS; lane w < W then
+    // builds agent w's vector (obs_emit, the code step_c runs) and its reward.
+    const int hslot = t_now % MSC_HISTORY, n_hist = t_now + 1 < MSC_HISTORY ? t_now + 1 : MSC_HISTORY;
+    const int RING = c.RING, tm = t_now % RING;
+    ScFcLds* Lf = reinterpret_cast<ScFcLds*>(Ll);
+    const bool lv = lvj[0];
+    const int i = w * K + skj[0];
+    const int64_t g = gi[0];
+    // loads first (one vmcnt for loads and stores): forecast, the 4 older history slots, the ring
+    int hv[MSC_HISTORY], rv[SC_FC_RING];
+    float fo = 0.0f;
+    int eltv = 0;
+    if (lv) {
+      fo = s.fc[g];
+      eltv = c.elt[i];
+#pragma unroll
+      for (int a = 1; a < MSC_HISTORY; a++) {  // age a: slot (t - a) mod 5
+        const int q = (t_now - a) % MSC_HISTORY;
+        hv[a] = a < n_hist ? s.hist[((int64_t)(q < 0 ? q + MSC_HISTORY : q) * WK + i) * E + e] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < SC_FC_RING; q++) rv[q] = FA ? Lra[q * 64 + lane] : (q < RING ? s.ring_q[((int64_t)i * RING + q) * E + e] : 0);
+    }
+    const int dh = home_done ? inc_h[0] : 0;  // this step's incoming home demand (step_a zeroed s.inc)
+    const int sh = home_done ? shh_h[0] : 0, sa = (inv0[0] - inv[0]) - sh;
+    hv[0] = dh;
+    float fcn = 0.0f, rm = 0.0f;
+    int pend = 0;
+    if (lv) {
+      s.hist[((int64_t)hslot * WK + i) * E + e] = dh;
+      fcn = 0.3f * (float)dh + 0.7f * fo;  // EMA forecast (f32)
+      s.fc[g] = fcn;
+      int hs = 0;
+#pragma unroll
+      for (int a = 0; a < MSC_HISTORY; a++) hs += a < n_hist ? hv[a] : 0;
+      rm = n_hist > 0 ? (float)hs / (float)n_hist : 0.0f;
+#pragma unroll
+      for (int q = 0; q < SC_FC_RING; q++) pend += rv[q];
+    }
+    // holding cost terms (reward_calculator.py:127-131), summed per warehouse in SKU order below
+    const int sk0 = skj[0];
+    double hterm = 0.0;
+    if (lv)
+      hterm = c.hold_per_sku ? (double)inv[0] * c.hold[sk0] : ((double)inv[0] * c.skw[sk0]) * c.hold_scalar;
+    Lf->v[FC_INV][lane] = inv[0];
+    Lf->v[FC_DH][lane] = dh;
+    Lf->v[FC_SH][lane] = sh;
+    Lf->v[FC_SA][lane] = sa;
+    Lf->v[FC_PEND][lane] = pend;
+    Lf->v[FC_ELT][lane] = eltv;
+    Lf->v[FC_FC][lane] = __float_as_int(fcn);
+    Lf->v[FC_RM][lane] = __float_as_int(rm);
+#pragma unroll
+    for (int q = 0; q < SC_FC_RING; q++) Lf->v[FC_RING + q][lane] = rv[q];
+#pragma unroll
+    for (int a = 0; a < MSC_HISTORY; a++) Lf->v[FC_HIST + a][lane] = hv[a];
+    Lw->dscr[lane] = hterm;
+    wave_sync();
+    const bool agent = sg == 0 && w < W;  // lane w builds agent w
+    const bool trunc = t_now + 1 >= c.T;
+    double rw = 0.0;
+    if (agent) {
+      double hold = 0.0;
+#pragma unroll
+      for (int j = 0; j < K; j++) hold += Lw->dscr[j * GW + w];
+      const double inb = FA ? inb_a : s.sc_inb[w * E + e];
+      rw = -((((hold + pen_w) + out_w) + inb) * c.scale);
+      if (dbg && info.costs) {
+        info.costs[(e * 4 + 0) * W + w] = hold;
+        info.costs[(e * 4 + 1) * W + w] = pen_w;
+        info.costs[(e * 4 + 2) * W + w] = out_w;
+        info.costs[(e * 4 + 3) * W + w] = inb;
+      }
+    }
+    Lov[lane] = rw;  // (the outbound partials are read)
+    wave_sync();
+    if (agent) {
+      double v = rw;
+      if (c.scope == MSC_SCOPE_TEAM) {  // team scope: sum over agents in agent order
+        v = 0.0;
+        for (int j = 0; j < W; j++) v += Lov[j];
+      }
+      io.rew[e * W + w] = (float)v;
+      if (io.rew64) io.rew64[e * W + w] = v;
+      // agent w's observation from the staged SKU values (lane sk * GW + w holds SKU sk)
+      int a_inv[K], a_dh[K], a_sh[K], a_sa[K], a_pend[K], a_elt[K];
+      float a_rm[K], a_fc[K];
+#pragma unroll
+      for (int sk = 0; sk < K; sk++) {
+        const int l = sk * GW + w;
+        a_inv[sk] = Lf->v[FC_INV][l];
+        a_dh[sk] = Lf->v[FC_DH][l];
+        a_sh[sk] = Lf->v[FC_SH][l];
+        a_sa[sk] = Lf->v[FC_SA][l];
+        a_pend[sk] = Lf->v[FC_PEND][l];
+        a_elt[sk] = Lf->v[FC_ELT][l];
+        a_fc[sk] = __int_as_float(Lf->v[FC_FC][l]);
+        a_rm[sk] = __int_as_float(Lf->v[FC_RM][l]);
+      }
+      // pipeline bucket l of SKU sk (_compute_pipeline): the order in ring slot q (age (t - q) mod
+      // RING) lands in bucket max(1, elt - age) - 1
+      auto pipe_at = [&](int l, int sk) -> int {
+        int v2 = 0;
+#pragma unroll
+        for (int q = 0; q < SC_FC_RING; q++) {
+          const int age = tm - q >= 0 ? tm - q : tm - q + RING;
+          const int b = a_elt[sk] - age > 1 ? a_elt[sk] - age - 1 : 0;
+          v2 += (q < RING && b == l) ? Lf->v[FC_RING + q][sk * GW + w] : 0;
+        }
+        return v2;
+      };
+      auto hist_at = [&](int a, int sk) -> int { return Lf->v[FC_HIST + a][sk * GW + w]; };
+      float* dst = trunc ? io.final_obs : io.obs;
+      if (dst) obs_emit<K>(c, w, n_hist, a_inv, a_dh, a_sh, a_sa, a_pend, a_elt, a_rm, a_fc, pipe_at, hist_at,
+                           dst + e * W * c.L);
+    }
+    // truncation: reset the env (one sequential RNG pass), then every agent's reset observation
+    if (trunc) {
+      if (lane == 0) reset_env<K>(c, s, e, 0, nullptr);
+      __builtin_amdgcn_s_waitcnt(0);  // (the reset's state stores have landed before they are read)
+      wave_sync();
+      if (agent) build_obs_agent<K>(c, s, e, w, 0, 0, nullptr, nullptr, 0, io.obs + e * W * c.L);
+    }
+    if (lane == 0) {
+      io.trunc[e] = trunc ? 1 : 0;
+      if (!trunc) s.t[e] = t_now + 1;
+    }
   }
 }
 
@@ -704,9 +927,14 @@ size_t alloc_scan_lds_bytes(const EnvConst& c) {
   const int GW = sc_gw(c.W), NS = sc_ns(c.K, GW);
   const size_t wave_b = NS > 1 ? sizeof(ScWaveLds<2>) : sizeof(ScWaveLds<1>);
   const size_t lost_b = GW > 8 ? sizeof(ScLostLds<16>) : sizeof(ScLostLds<8>);
+  // (the fused phase C stages its inputs where the deferred regions were)
+  const size_t tail_b = c.fuse_c ? (lost_b > sizeof(ScFcLds) ? lost_b : sizeof(ScFcLds)) : (c.scan_defer ? lost_b : 0);
   return (alloc_scan_tab(c, GW) ? sc_tab_bytes(c.R, GW) : 0) + sizeof(int32_t) * ((c.R + 3) & ~3) +
-         SC_WAVES * wave_b + (c.scan_defer ? SC_WAVES * lost_b : 0);
+         SC_WAVES * wave_b + SC_WAVES * tail_b + (c.fuse_a ? (size_t)SC_WAVES * SC_FC_RING * 64 * sizeof(int32_t) : 0);
 }
+// phase C fused into the scan allocator: one slot per lane (<= 8 warehouses), pending rings of at
+// most SC_FC_RING slots
+bool alloc_scan_fuse_supported(int W, int K, int RING) { return W <= 8 && K <= 6 && RING <= SC_FC_RING; }
 // <= 8 warehouses with <= 6 SKUs (one slot per lane), 9-16 warehouses with <= 6 SKUs (two slots
 // above 4 SKUs)
 bool alloc_scan_supported(int W, int K) { return W <= 16 && K <= 6; }
@@ -716,10 +944,23 @@ static hipError_t launch_scan_k(const EnvConst& c, const DevEnv* d, const StepIO
   using KFn = void (*)(const DevEnv*, StepIO);
   const int GW = sc_gw(c.W);
   const bool t = alloc_scan_tab(c, GW);
-  KFn f = GW == 2 ? (t ? (KFn)alloc_scan_kernel<K, 2, true> : (KFn)alloc_scan_kernel<K, 2, false>)
-        : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true> : (KFn)alloc_scan_kernel<K, 4, false>)
-        : GW == 8 ? (t ? (KFn)alloc_scan_kernel<K, 8, true> : (KFn)alloc_scan_kernel<K, 8, false>)
-                  : (t ? (KFn)alloc_scan_kernel<K, 16, true> : (KFn)alloc_scan_kernel<K, 16, false>);
+  KFn f;
+  if (c.fuse_c && c.fuse_a) {
+    f = GW == 2 ? (t ? (KFn)alloc_scan_kernel<K, 2, true, true, true> : (KFn)alloc_scan_kernel<K, 2, false, true, true>)
+      : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true, true, true> : (KFn)alloc_scan_kernel<K, 4, false, true, true>)
+                : (t ? (KFn)alloc_scan_kernel<K, 8, true, true, true> : (KFn)alloc_scan_kernel<K, 8, false, true, true>);
+    if (GW > 8) return hipErrorInvalidValue;
+  } else if (c.fuse_c) {
+    f = GW == 2 ? (t ? (KFn)alloc_scan_kernel<K, 2, true, true> : (KFn)alloc_scan_kernel<K, 2, false, true>)
+      : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true, true> : (KFn)alloc_scan_kernel<K, 4, false, true>)
+                : (t ? (KFn)alloc_scan_kernel<K, 8, true, true> : (KFn)alloc_scan_kernel<K, 8, false, true>);
+    if (GW > 8) return hipErrorInvalidValue;
+  } else {
+    f = GW == 2 ? (t ? (KFn)alloc_scan_kernel<K, 2, true> : (KFn)alloc_scan_kernel<K, 2, false>)
+      : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true> : (KFn)alloc_scan_kernel<K, 4, false>)
+      : GW == 8 ? (t ? (KFn)alloc_scan_kernel<K, 8, true> : (KFn)alloc_scan_kernel<K, 8, false>)
+                : (t ? (KFn)alloc_scan_kernel<K, 16, true> : (KFn)alloc_scan_kernel<K, 16, false>);
+  }
   const size_t lds = alloc_scan_lds_bytes(c);
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -473,6 +473,19 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     if (c.alloc_impl == 1 && !al_env && W <= 8 && alloc_scan_supported(W, K)) c.alloc_impl = 2;
     if (al_env && strcmp(al_env, "scan") == 0) c.alloc_impl = alloc_scan_supported(W, K) ? 2 : 1;
     c.scan_defer = 1;
+    // phase C inside the scan allocator (one env per wave: its obs, rewards and state updates from the
+    // allocation's registers; no step_c launch). MSC_FUSE_C=0 keeps the step_c kernel.
+    c.fuse_c = c.alloc_impl == 2 && alloc_scan_fuse_supported(W, K, RING) ? 1 : 0;
+    if (const char* fc = getenv("MSC_FUSE_C")) c.fuse_c = c.fuse_c && atoi(fc) != 0 ? 1 : 0;
+    // phase A too when it has no per-env RNG work (fixed lead times; Poisson demand: the empirical
+    // sampler draws its window start in phase A). MSC_FUSE_A=0 keeps the step_a kernel.
+    c.fuse_a = c.fuse_c && d->lead_type != MSC_LEAD_STOCHASTIC && d->demand_type == MSC_DEMAND_POISSON ? 1 : 0;
+    c.sb_gw = 0;
+    if (const char* g = getenv("MSC_SB_GW")) {
+      const int v = atoi(g);
+      c.sb_gw = (v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
+    }
+    if (const char* fa = getenv("MSC_FUSE_A")) c.fuse_a = c.fuse_a && atoi(fa) != 0 ? 1 : 0;
     {
       // step_b's block tables ({of, ov} rows [2][R][W] f64 + closest [R] i32) in LDS: when small
       // (16 KB, room for the blocks of the pipelined demand kernel beside the step), or, with
@@ -481,7 +494,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       // record windows + 65 KB of tables); otherwise each region change reads its cost row from L2
       int ncu = 256;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
-      const int gw = W <= 2 ? 2 : W <= 4 ? 4 : W <= 8 ? 8 : W <= 16 ? 16 : 32;
+      int gw = W <= 2 ? 2 : W <= 4 ? 4 : W <= 8 ? 8 : W <= 16 ? 16 : 32;
+      if (const char* g = getenv("MSC_SB_GW")) gw = atoi(g) > gw && atoi(g) <= 32 ? atoi(g) : gw;
       const int64_t blocks = (n_envs * gw + 255) / 256, per_cu = (blocks + ncu - 1) / ncu;
       const size_t tab = (size_t)2 * R * W * sizeof(double) + (size_t)R * sizeof(int32_t);
       const size_t blk = (size_t)4 * 2 * 128 * 16 + tab;  // 4 waves x 2 windows x SB_REC records + tables

@@ -48,6 +48,9 @@ struct EnvConst {
   int32_t scan_defer;   // alloc_scan_kernel: lost-sales shares deferred to a post-pass (MSC_SCAN_DEFER=0: inline)
   int32_t demand_ptrs;  // 1: some Poisson rate >= 10 (numpy's PTRS branch): the sequential sampler demand_seq_kernel
   int32_t sb_tab;       // 1: step_b_kernel stages the {of, ov} rows and closest warehouses in LDS (its TAB form)
+  int32_t fuse_c;       // 1: the scan allocator also runs phase C (step_c_kernel's work) for its env
+  int32_t fuse_a;       // 1: ... and phase A (step_a_kernel's work; fixed lead times, Poisson demand)
+  int32_t sb_gw;        // step_b lane-group width forced wider than the warehouse count (MSC_SB_GW; 0: by W)
   uint32_t flags;
   int64_t E;
   int64_t ea_cap;       // episode-ahead demand: order records per (slot, env) episode
@@ -198,6 +201,7 @@ hipError_t launch_demand_ea(const EnvConst& c, const DevEnv* d, const EaLaunch& 
 hipError_t launch_ea_materialize(const EnvConst& c, const DevEnv* d, int slot, int t_done, hipStream_t st);
 // alloc_scan.hip
 hipError_t launch_alloc_scan(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st);
+bool alloc_scan_fuse_supported(int W, int K, int RING);
 bool alloc_scan_supported(int W, int K);
 constexpr int SORT_BUCKETS = 1024;
 // alloc_kernels.hip

@@ -20,7 +20,9 @@ def _set_alloc(monkeypatch, param):
     # "<impl>[_<opt>...]": impl lane / lane2 / lane4 (one env per lane, 1 / 2 / 4 lanes per env),
     # group (one env per lane group), scan (one env per wave, prefix scan over the cost ranking);
     # opts sorted / unsorted (group kernel's visiting order), ea0 / ea1 (episode-ahead demand off /
-    # on; default: on for the scan kernel, the library's choice for group, off for lane)
+    # on; default: on for the scan kernel, the library's choice for group, off for lane), nofc (the
+    # scan allocator without its fused phases A and C: the step_a / step_c kernels run), nofa (phase C
+    # fused, phase A in step_a)
     impl, *opts = param.split("_")
     monkeypatch.setenv("MSC_ALLOC_IMPL", "lane" if impl.startswith("lane") else impl)
     monkeypatch.setenv("MSC_ALLOC_LPE", impl[4:] if impl.startswith("lane") and impl[4:] else "0")
@@ -41,6 +43,15 @@ def _set_alloc(monkeypatch, param):
         monkeypatch.setenv("MSC_OBS_STAGE", "1")
     else:
         monkeypatch.delenv("MSC_OBS_STAGE", raising=False)
+    # the scan allocator runs phase C itself (MSC_FUSE_C, default on); "nofc" keeps the step_c kernel
+    if "nofc" in opts:
+        monkeypatch.setenv("MSC_FUSE_C", "0")
+    else:
+        monkeypatch.delenv("MSC_FUSE_C", raising=False)
+    if "nofa" in opts:  # phase C fused, phase A in the step_a kernel
+        monkeypatch.setenv("MSC_FUSE_A", "0")
+    else:
+        monkeypatch.delenv("MSC_FUSE_A", raising=False)
     ea = "0" if "ea0" in opts or impl.startswith("lane") else "1" if ("ea1" in opts or impl == "scan") else None
     if ea is None:
         monkeypatch.delenv("MSC_EA", raising=False)
@@ -48,7 +59,7 @@ def _set_alloc(monkeypatch, param):
         monkeypatch.setenv("MSC_EA", ea)
 
 
-@pytest.fixture(params=["lane", "group", "group_sorted", "scan", "scan_ea0"])
+@pytest.fixture(params=["lane", "group", "group_sorted", "scan", "scan_ea0", "scan_nofc", "scan_nofa"])
 def alloc_impl(request, monkeypatch):
     # every phase-B allocation kernel (one env per lane / per lane group / per wave) against the same
     # references, with and without episode-ahead demand; msc_env_create picks by shape otherwise
@@ -56,7 +67,8 @@ def alloc_impl(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lane", "lane2", "lane4", "group", "group_sorted", "group_unsorted_ea1", "scan", "scan_ea0"])
+@pytest.fixture(params=["lane", "lane2", "lane4", "group", "group_sorted", "group_unsorted_ea1", "scan", "scan_ea0",
+                        "scan_nofc"])
 def alloc_impl_lpe(request, monkeypatch):
     # as alloc_impl, plus the lane kernel's 2 / 4 lanes-per-env forms (A/B; >= 8 warehouses)
     _set_alloc(monkeypatch, request.param)
