@@ -475,11 +475,13 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     c.scan_defer = 1;
     // phase C inside the scan allocator (one env per wave: its obs, rewards and state updates from the
     // allocation's registers; no step_c launch). MSC_FUSE_C=0 keeps the step_c kernel.
-    c.fuse_c = c.alloc_impl == 2 && alloc_scan_fuse_supported(W, K, RING) ? 1 : 0;
+    c.fuse_c = c.alloc_impl == 2 ? (alloc_scan_fuse_supported(W, K, RING) ? 1 : 0)
+             : c.alloc_impl == 1 ? (K <= 8 && RING <= 4 ? 1 : 0)  // the group allocator's (step_b_phase_c)
+             : 0;
     if (const char* fc = getenv("MSC_FUSE_C")) c.fuse_c = c.fuse_c && atoi(fc) != 0 ? 1 : 0;
     // phase A too when it has no per-env RNG work (fixed lead times; Poisson demand: the empirical
     // sampler draws its window start in phase A). MSC_FUSE_A=0 keeps the step_a kernel.
-    c.fuse_a = c.fuse_c && d->lead_type != MSC_LEAD_STOCHASTIC && d->demand_type == MSC_DEMAND_POISSON ? 1 : 0;
+    c.fuse_a = c.alloc_impl == 2 && c.fuse_c && d->lead_type != MSC_LEAD_STOCHASTIC && d->demand_type == MSC_DEMAND_POISSON ? 1 : 0;
     c.sb_gw = 0;
     if (const char* g = getenv("MSC_SB_GW")) {
       const int v = atoi(g);

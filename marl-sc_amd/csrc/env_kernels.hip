@@ -1056,6 +1056,117 @@ __global__ __launch_bounds__(1024) void alloc_sort_kernel(const DevEnv* __restri
 }
 #endif
 
+// Phase C fused into the group allocator (c.fuse_c; step_c_kernel's work, multi_env.py:307-327,
+// 747-793, reward_calculator.py:96-190): lane w of env e's group is agent w, its SKUs' inventory in
+// registers after the allocation; the history, forecast and observation of agent w, the reward (team
+// scope: the group's sum in agent order), and the in-kernel reset at truncation (the group's lane 0).
+// This lane's home-region stores of the allocation (s.inc, s.sc_shh) are read back after a wait.
+constexpr int SB_FC_RING = 4;  // pending-ring slots held in registers (lead times <= 3)
+template <int K, int GW>
+__device__ __forceinline__ void step_b_phase_c(const EnvConst& c, const EnvState& s, const StepIO& io, int64_t e, int w,
+                                               bool ev, bool wl, int gbase, bool home_done, const int (&inv)[K],
+                                               double pen, double out) {
+  const int64_t E = c.E;
+  const int W = c.W, WK = W * K, RING = c.RING;
+  const bool on = ev && wl;
+  const int t_now = ev ? s.t[e] : 0;
+  const int hslot = t_now % MSC_HISTORY, n_hist = t_now + 1 < MSC_HISTORY ? t_now + 1 : MSC_HISTORY;
+  const int tm = t_now % RING;
+  const bool trunc = ev && t_now + 1 >= c.T;
+  __builtin_amdgcn_s_waitcnt(0);  // (the allocation's stores of this lane have landed)
+  int a_inv[K], a_dh[K], a_sh[K], a_sa[K], a_pend[K], a_elt[K], hv[K][MSC_HISTORY], rv[K][SB_FC_RING];
+  float a_rm[K], a_fc[K], fo[K];
+  double hold = 0.0;
+  if (on) {
+    // every load first (one vmcnt for loads and stores)
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      const int64_t g = (int64_t)i * E + e;
+      a_inv[sk] = inv[sk];
+      a_sa[sk] = s.inv[g] - inv[sk];  // shipped this step (the inventory drop); minus home below
+      a_dh[sk] = s.inc[g];            // this step's incoming home demand (0 unless the home region)
+      a_sh[sk] = home_done ? s.sc_shh[g] : 0;
+      fo[sk] = s.fc[g];
+      a_elt[sk] = c.elt[i];
+#pragma unroll
+      for (int a = 1; a < MSC_HISTORY; a++) {
+        const int q = (t_now - a) % MSC_HISTORY;
+        hv[sk][a] = a < n_hist ? s.hist[((int64_t)(q < 0 ? q + MSC_HISTORY : q) * WK + i) * E + e] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < SB_FC_RING; q++) rv[sk][q] = q < RING ? s.ring_q[((int64_t)i * RING + q) * E + e] : 0;
+    }
+#pragma unroll
+    for (int sk = 0; sk < K; sk++) {
+      const int i = w * K + sk;
+      const int64_t g = (int64_t)i * E + e;
+      a_sa[sk] -= a_sh[sk];
+      hv[sk][0] = a_dh[sk];
+      s.hist[((int64_t)hslot * WK + i) * E + e] = a_dh[sk];
+      a_fc[sk] = 0.3f * (float)a_dh[sk] + 0.7f * fo[sk];  // EMA forecast (f32)
+      s.fc[g] = a_fc[sk];
+      s.inv[g] = inv[sk];
+      int hs = 0, pend = 0;
+#pragma unroll
+      for (int a = 0; a < MSC_HISTORY; a++) hs += a < n_hist ? hv[sk][a] : 0;
+      a_rm[sk] = n_hist > 0 ? (float)hs / (float)n_hist : 0.0f;
+#pragma unroll
+      for (int q = 0; q < SB_FC_RING; q++) pend += rv[sk][q];
+      a_pend[sk] = pend;
+      hold += c.hold_per_sku ? (double)inv[sk] * c.hold[sk] : ((double)inv[sk] * c.skw[sk]) * c.hold_scalar;
+    }
+  }
+  const double inb = on ? s.sc_inb[w * E + e] : 0.0;
+  const double rw = -((((hold + pen) + out) + inb) * c.scale);
+  if (on && io.has_info && io.info.costs) {
+    io.info.costs[(e * 4 + 0) * W + w] = hold;
+    io.info.costs[(e * 4 + 1) * W + w] = pen;
+    io.info.costs[(e * 4 + 2) * W + w] = out;
+    io.info.costs[(e * 4 + 3) * W + w] = inb;
+  }
+  double v = rw;
+  if (c.scope == MSC_SCOPE_TEAM) {  // (uniform) the group's sum in agent order, every lane active
+    v = 0.0;
+    for (int j = 0; j < W; j++) v += __shfl(rw, gbase + j);
+  }
+  if (on) {
+    io.rew[e * W + w] = (float)v;
+    if (io.rew64) io.rew64[e * W + w] = v;
+    auto pipe_at = [&](int l, int sk) -> int {  // bucket max(1, elt - age) - 1 of ring slot q
+      int v2 = 0;
+#pragma unroll
+      for (int q = 0; q < SB_FC_RING; q++) {
+        const int age = tm - q >= 0 ? tm - q : tm - q + RING;
+        const int b = a_elt[sk] - age > 1 ? a_elt[sk] - age - 1 : 0;
+        v2 += (q < RING && b == l) ? rv[sk][q] : 0;
+      }
+      return v2;
+    };
+    auto hist_at = [&](int a, int sk) -> int {
+      int v2 = 0;
+#pragma unroll
+      for (int q = 0; q < MSC_HISTORY; q++) v2 = q == a ? hv[sk][q] : v2;
+      return v2;
+    };
+    float* dst = trunc ? io.final_obs : io.obs;
+    if (dst) obs_emit<K>(c, w, n_hist, a_inv, a_dh, a_sh, a_sa, a_pend, a_elt, a_rm, a_fc, pipe_at, hist_at, dst + e * W * c.L);
+  }
+  // truncation: the group's lane 0 resets the env, then every agent's reset observation
+  if (__ballot(trunc) != 0ull) {
+    if (trunc && w == 0) reset_env<K>(c, s, e, 0, nullptr);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (trunc && wl) build_obs_agent<K>(c, s, e, w, 0, 0, nullptr, nullptr, 0, io.obs + e * W * c.L);
+  }
+  if (ev && w == 0) {
+    io.trunc[e] = trunc ? 1 : 0;
+    if (!trunc) s.t[e] = t_now + 1;
+  }
+}
+
 // (above 8 SKUs the K-wide register arrays of a lane need the larger budget of 2 waves per SIMD)
 template <int K, int GW, bool DBG, bool TAB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : GW >= 16 ? MSC_SB_WPE16 : MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
@@ -1387,6 +1498,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
   PROF_FLUSH(13, q_iter);
   PROF_FLUSH(14, q_nfin);
   PROF_FLUSH(15, 1ull);
+  if constexpr (K <= 8) {
+    if (c.fuse_c) {  // (uniform) phase C here: the step_c kernel is not launched
+      step_b_phase_c<K, GW>(c, s, io, e, w, ev, wl, gbase, home_done, inv, pen, out);
+      return;
+    }
+  }
   if (ev && wl) {
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
@@ -1743,7 +1860,7 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     }
     hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), lds_b, st, d, io);
   }
-  if (c.alloc_impl == 2 && c.fuse_c) return hipGetLastError();  // (phase C ran inside the scan allocator)
+  if (c.fuse_c && c.alloc_impl != 0) return hipGetLastError();  // (phase C ran inside the allocator)
   const int stage_w = c.obs_stage ? (c.W + (c.obs_stage > 1 ? c.obs_stage : 1) - 1) / (c.obs_stage > 1 ? c.obs_stage : 1) : 0;
   const size_t lds_c = (size_t)c.W * BS * sizeof(double) +
                        (c.obs_stage ? (size_t)BS * ((stage_w * c.L) | 1) * sizeof(float) + BS * sizeof(int32_t) : 0);
