@@ -199,6 +199,155 @@ __device__ __forceinline__ T sc_readlane(T v, int l) {
   }
 }
 
+// Fused phase C: the observation of agent w written by lane (sk, w) -- SKU sk's value of every
+// per-SKU feature block and, on lane sk == 0, the aggregates and the one-hot entries -- instead of
+// one lane per agent (obs_emit, the same arithmetic value by value: _build_local_obs /
+// _feature_block, multi_env.py:577-745). The agent's inputs are the staged ones (ScFcLds, lane
+// s * GW + w); o points at the agent's vector.
+template <int K, int GW>
+__device__ __forceinline__ void fc_obs_lane(const EnvConst& c, const ScFcLds* Lf, int w, int sk, int tm, int n_hist,
+                                            float* o) {
+  const int W = c.W, Lmax = c.Lmax, RING = c.RING;
+  const uint32_t f = c.flags;
+  const bool ratio = c.norm == MSC_OBS_RATIO, meanstd = c.norm == MSC_OBS_MEANSTD;
+  const double eps = 1e-8;
+  const float epsf = 1e-8f;
+  const int l0 = sk * GW + w;
+  const int inv = Lf->v[FC_INV][l0], dh = Lf->v[FC_DH][l0], sh = Lf->v[FC_SH][l0], sa = Lf->v[FC_SA][l0];
+  const int pend = Lf->v[FC_PEND][l0], elt = Lf->v[FC_ELT][l0];
+  const float fc = __int_as_float(Lf->v[FC_FC][l0]), rm = __int_as_float(Lf->v[FC_RM][l0]);
+  // the agent's totals (obs_emit's sums, SKU order)
+  double inv_total = 0.0, shipped_total = 0.0, sa_total = 0.0;
+  float dh_total = 0.0f, rm_a[K], fc_a[K];
+  int pend_total = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int l = k * GW + w;
+    inv_total += (double)Lf->v[FC_INV][l];
+    dh_total += (float)Lf->v[FC_DH][l];
+    shipped_total += (double)(Lf->v[FC_SH][l] + Lf->v[FC_SA][l]);
+    sa_total += (double)Lf->v[FC_SA][l];
+    pend_total += Lf->v[FC_PEND][l];
+    rm_a[k] = __int_as_float(Lf->v[FC_RM][l]);
+    fc_a[k] = __int_as_float(Lf->v[FC_FC][l]);
+  }
+  const float rm_total = np_sum_f32<K>(rm_a);
+  const float fc_total = np_sum_f32<K>(fc_a);
+  const int base = c.wid ? W : 0;
+  auto put = [&](int j, double v) {  // feature j (the one-hot excluded)
+    float x = (float)v;
+    if (meanstd) x = (x - c.obs_mean[j]) / c.obs_std[j];
+    o[base + j] = x;
+  };
+  const bool lead = sk == 0;  // writes the aggregates and the one-hot
+  if (c.wid)
+    for (int k = sk; k < W; k += K) o[k] = (k == w) ? 1.0f : 0.0f;
+  int j0 = 0;  // first feature index of the current block
+  if (f & MSC_F_INVENTORY) {
+    put(j0 + sk, ratio ? (double)inv / (inv_total + eps) : (double)inv);
+    j0 += K;
+    if (f & MSC_F_INVENTORY_AGG) {
+      if (lead) put(j0, (double)(float)inv_total);
+      j0++;
+    }
+  }
+  if (f & MSC_F_PIPELINE) {
+    const float den = (float)((double)pend_total + eps);
+    for (int l = 0; l < Lmax; l++) {
+      // bucket l of this SKU: the order in ring slot q (age (t - q) mod RING) lands in bucket
+      // max(1, elt - age) - 1 (_compute_pipeline, multi_env.py:956-966)
+      int pv = 0;
+#pragma unroll
+      for (int q = 0; q < SC_FC_RING; q++) {
+        const int age = tm - q >= 0 ? tm - q : tm - q + RING;
+        const int bk = elt - age > 1 ? elt - age - 1 : 0;
+        pv += (q < RING && bk == l) ? Lf->v[FC_RING + q][l0] : 0;
+      }
+      const float v = (float)pv;
+      put(j0 + l * K + sk, ratio ? (double)(v / den) : (double)v);
+    }
+    j0 += Lmax * K;
+    if (f & MSC_F_PIPELINE_AGG) {
+      if (lead) put(j0, (double)pend_total);
+      j0++;
+    }
+  }
+  if (f & MSC_F_INCOMING_HOME) {
+    const float den = dh_total + epsf;
+    put(j0 + sk, ratio ? (double)((float)dh / den) : (double)dh);
+    j0 += K;
+    if (f & MSC_F_INCOMING_HOME_AGG) {
+      if (lead) put(j0, (double)dh_total);
+      j0++;
+    }
+  }
+  if (f & MSC_F_SHIPPED_HOME) {
+    const double den = (double)(dh_total + epsf);
+    put(j0 + sk, ratio ? (double)sh / den : (double)sh);
+    j0 += K;
+  }
+  if (f & MSC_F_SHIPPED_AWAY) {
+    put(j0 + sk, ratio ? (double)sa / (shipped_total + eps) : (double)sa);
+    j0 += K;
+    if (f & MSC_F_SHIPPED_AWAY_AGG) {
+      if (lead) put(j0, (double)(float)(sa_total / (shipped_total + eps)));
+      j0++;
+    }
+  }
+  if (f & MSC_F_STOCKOUT) {
+    const float den = dh_total + epsf;
+    const float so = (float)(dh - sh > 0 ? dh - sh : 0);
+    put(j0 + sk, ratio ? (double)(so / den) : (double)so);
+    j0 += K;
+  }
+  if (f & MSC_F_ROLLING_MEAN) {
+    const float den = rm_total + epsf;
+    put(j0 + sk, ratio ? (double)(rm / den) : (double)rm);
+    j0 += K;
+    if (f & MSC_F_ROLLING_MEAN_AGG) {
+      if (lead) put(j0, (double)rm_total);
+      j0++;
+    }
+  }
+  if (f & MSC_F_FORECAST) {
+    const float den = fc_total + epsf;
+    put(j0 + sk, ratio ? (double)(fc / den) : (double)fc);
+    j0 += K;
+    if (f & MSC_F_FORECAST_AGG) {
+      if (lead) put(j0, (double)fc_total);
+      j0++;
+    }
+  }
+  if (f & MSC_F_DAYS_OF_SUPPLY) {
+    put(j0 + sk, (double)(float)((double)inv / (double)(rm > 1.0f ? rm : 1.0f)));
+    j0 += K;
+  }
+  if (f & MSC_F_NET_POSITION) {
+    put(j0 + sk, (double)(float)(((double)inv + (double)pend) - (double)fc * (double)elt));
+    j0 += K;
+  }
+  if (f & MSC_F_DEMAND_VARIABILITY) {
+    float sd = 0.0f;
+    if (n_hist > 1) {  // oldest first, as the deque (multi_env.py:776-789)
+      float sum = 0.0f;
+      for (int h = 0; h < n_hist; h++) sum += (float)Lf->v[FC_HIST + (n_hist - 1 - h)][l0];
+      const float mean = sum / (float)n_hist;
+      float ss = 0.0f;
+      for (int h = 0; h < n_hist; h++) {
+        const float d = (float)Lf->v[FC_HIST + (n_hist - 1 - h)][l0] - mean;
+        ss += d * d;
+      }
+      sd = sqrtf(ss / (float)n_hist);
+    }
+    put(j0 + sk, (double)sd);
+    j0 += K;
+  }
+  if (f & MSC_F_DEMAND_HISTORY) {
+    for (int h = 0; h < MSC_HISTORY; h++) put(j0 + h * K + sk, (double)(h < n_hist ? Lf->v[FC_HIST + h][l0] : 0));
+    j0 += MSC_HISTORY * K;
+  }
+}
+
 // Orders of one region with the same cost ranking form a batch: greedy fills of consecutive orders
 // over one ranking are the fills of their running demand total, so order k of a batch takes
 //     f_{k,p,s} = a_k - a_{k-1},  a_k = min(inv_{p,s}, max(0, D_{k,s} - sum_{q<p} inv_{q,s})),
@@ -876,38 +1025,11 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
       }
       io.rew[e * W + w] = (float)v;
       if (io.rew64) io.rew64[e * W + w] = v;
-      // agent w's observation from the staged SKU values (lane sk * GW + w holds SKU sk)
-      int a_inv[K], a_dh[K], a_sh[K], a_sa[K], a_pend[K], a_elt[K];
-      float a_rm[K], a_fc[K];
-#pragma unroll
-      for (int sk = 0; sk < K; sk++) {
-        const int l = sk * GW + w;
-        a_inv[sk] = Lf->v[FC_INV][l];
-        a_dh[sk] = Lf->v[FC_DH][l];
-        a_sh[sk] = Lf->v[FC_SH][l];
-        a_sa[sk] = Lf->v[FC_SA][l];
-        a_pend[sk] = Lf->v[FC_PEND][l];
-        a_elt[sk] = Lf->v[FC_ELT][l];
-        a_fc[sk] = __int_as_float(Lf->v[FC_FC][l]);
-        a_rm[sk] = __int_as_float(Lf->v[FC_RM][l]);
-      }
-      // pipeline bucket l of SKU sk (_compute_pipeline): the order in ring slot q (age (t - q) mod
-      // RING) lands in bucket max(1, elt - age) - 1
-      auto pipe_at = [&](int l, int sk) -> int {
-        int v2 = 0;
-#pragma unroll
-        for (int q = 0; q < SC_FC_RING; q++) {
-          const int age = tm - q >= 0 ? tm - q : tm - q + RING;
-          const int b = a_elt[sk] - age > 1 ? a_elt[sk] - age - 1 : 0;
-          v2 += (q < RING && b == l) ? Lf->v[FC_RING + q][sk * GW + w] : 0;
-        }
-        return v2;
-      };
-      auto hist_at = [&](int a, int sk) -> int { return Lf->v[FC_HIST + a][sk * GW + w]; };
-      float* dst = trunc ? io.final_obs : io.obs;
-      if (dst) obs_emit<K>(c, w, n_hist, a_inv, a_dh, a_sh, a_sa, a_pend, a_elt, a_rm, a_fc, pipe_at, hist_at,
-                           dst + e * W * c.L);
     }
+    // the observation, every lane (s, w) writing SKU s's values of agent w (obs_emit's arithmetic
+    // value by value; the agent's totals from the staged SKU values, in SKU order)
+    float* dst = trunc ? io.final_obs : io.obs;
+    if (dst && lv) fc_obs_lane<K, GW>(c, Lf, w, sk0, tm, n_hist, dst + (e * W + w) * (int64_t)c.L);
     // truncation: reset the env (one sequential RNG pass), then every agent's reset observation
     if (trunc) {
       if (lane == 0) reset_env<K>(c, s, e, 0, nullptr);
