@@ -72,7 +72,13 @@ constexpr int SC_WIN = 64;   // orders ranked per window (one per lane)
 // unfulfilled units per SKU; the shares and the lost-sales sums run after the order loop, eight regions
 // per pass (lane = region slot x warehouse) and then one multiply-add per region and (SKU, warehouse)
 // lane, in region order (the reference's summation order, lost_sales_handler.py:113-148 / :170-210).
-constexpr int SC_LR = 64;  // deferred regions per flush
+// deferred regions per flush: 16 (a 1.25-KB block per wave; 64 in rounds 3-4, 5 KB) leaves more of a
+// CU's 160 KB of LDS to the episode-ahead generation's blocks (37 KB each) running beside the scan
+// blocks at configs[1]: C2 205.5 -> 208.4 M agent-steps/s (profiles/r05/ab_scan_lds.txt)
+#ifndef MSC_SC_LR
+#define MSC_SC_LR 16
+#endif
+constexpr int SC_LR = MSC_SC_LR;
 
 // LDS per wave: the window's order records, epilogue scratch (64 entries per SKU slot, see NS)
 template <int NS>
@@ -95,8 +101,9 @@ struct ScLostLds {
 // fused phase C: the per-(SKU, warehouse) inputs of the observation builder, [field][s * GW + w]
 // (aliases the deferred-region block, flushed by then; allocated as the larger of the two)
 constexpr int SC_FC_RING = 4;  // pending-ring slots staged (lead times <= 3)
-enum : int { FC_INV, FC_DH, FC_SH, FC_SA, FC_PEND, FC_ELT, FC_FC, FC_RM, FC_RING, FC_HIST = FC_RING + SC_FC_RING,
-             FC_NF = FC_HIST + MSC_HISTORY };
+// (the fields an agent's totals read across its SKU lanes; the ring, history and lead time a lane
+// reads only for its own SKU stay in its registers)
+enum : int { FC_INV, FC_DH, FC_SH, FC_SA, FC_PEND, FC_FC, FC_RM, FC_NF };
 struct ScFcLds {
   int32_t v[FC_NF][64];
 };
@@ -199,6 +206,12 @@ __device__ __forceinline__ T sc_readlane(T v, int l) {
   }
 }
 
+__device__ __forceinline__ int hist_of(const int (&hv)[MSC_HISTORY], int a) {
+  int v = 0;
+#pragma unroll
+  for (int q = 0; q < MSC_HISTORY; q++) v = q == a ? hv[q] : v;
+  return v;
+}
 // Fused phase C: the observation of agent w written by lane (sk, w) -- SKU sk's value of every
 // per-SKU feature block and, on lane sk == 0, the aggregates and the one-hot entries -- instead of
 // one lane per agent (obs_emit, the same arithmetic value by value: _build_local_obs /
@@ -206,6 +219,7 @@ __device__ __forceinline__ T sc_readlane(T v, int l) {
 // s * GW + w); o points at the agent's vector.
 template <int K, int GW>
 __device__ __forceinline__ void fc_obs_lane(const EnvConst& c, const ScFcLds* Lf, int w, int sk, int tm, int n_hist,
+                                            int elt, const int (&rv)[SC_FC_RING], const int (&hv)[MSC_HISTORY],
                                             float* o) {
   const int W = c.W, Lmax = c.Lmax, RING = c.RING;
   const uint32_t f = c.flags;
@@ -214,7 +228,7 @@ __device__ __forceinline__ void fc_obs_lane(const EnvConst& c, const ScFcLds* Lf
   const float epsf = 1e-8f;
   const int l0 = sk * GW + w;
   const int inv = Lf->v[FC_INV][l0], dh = Lf->v[FC_DH][l0], sh = Lf->v[FC_SH][l0], sa = Lf->v[FC_SA][l0];
-  const int pend = Lf->v[FC_PEND][l0], elt = Lf->v[FC_ELT][l0];
+  const int pend = Lf->v[FC_PEND][l0];
   const float fc = __int_as_float(Lf->v[FC_FC][l0]), rm = __int_as_float(Lf->v[FC_RM][l0]);
   // the agent's totals (obs_emit's sums, SKU order)
   double inv_total = 0.0, shipped_total = 0.0, sa_total = 0.0;
@@ -261,7 +275,7 @@ __device__ __forceinline__ void fc_obs_lane(const EnvConst& c, const ScFcLds* Lf
       for (int q = 0; q < SC_FC_RING; q++) {
         const int age = tm - q >= 0 ? tm - q : tm - q + RING;
         const int bk = elt - age > 1 ? elt - age - 1 : 0;
-        pv += (q < RING && bk == l) ? Lf->v[FC_RING + q][l0] : 0;
+        pv += (q < RING && bk == l) ? rv[q] : 0;
       }
       const float v = (float)pv;
       put(j0 + l * K + sk, ratio ? (double)(v / den) : (double)v);
@@ -330,11 +344,11 @@ __device__ __forceinline__ void fc_obs_lane(const EnvConst& c, const ScFcLds* Lf
     float sd = 0.0f;
     if (n_hist > 1) {  // oldest first, as the deque (multi_env.py:776-789)
       float sum = 0.0f;
-      for (int h = 0; h < n_hist; h++) sum += (float)Lf->v[FC_HIST + (n_hist - 1 - h)][l0];
+      for (int h = 0; h < n_hist; h++) sum += (float)hist_of(hv, n_hist - 1 - h);
       const float mean = sum / (float)n_hist;
       float ss = 0.0f;
       for (int h = 0; h < n_hist; h++) {
-        const float d = (float)Lf->v[FC_HIST + (n_hist - 1 - h)][l0] - mean;
+        const float d = (float)hist_of(hv, n_hist - 1 - h) - mean;
         ss += d * d;
       }
       sd = sqrtf(ss / (float)n_hist);
@@ -343,7 +357,7 @@ __device__ __forceinline__ void fc_obs_lane(const EnvConst& c, const ScFcLds* Lf
     j0 += K;
   }
   if (f & MSC_F_DEMAND_HISTORY) {
-    for (int h = 0; h < MSC_HISTORY; h++) put(j0 + h * K + sk, (double)(h < n_hist ? Lf->v[FC_HIST + h][l0] : 0));
+    for (int h = 0; h < MSC_HISTORY; h++) put(j0 + h * K + sk, (double)(h < n_hist ? hist_of(hv, h) : 0));
     j0 += MSC_HISTORY * K;
   }
 }
@@ -400,10 +414,6 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
   ScLostLds<GW>* Ll =
       reinterpret_cast<ScLostLds<GW>*>(reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) + wave;
   constexpr int LA = ScLostLds<GW>::LA;
-  // FA: the ring after phase A, [q][lane], after the tail blocks (their size: alloc_scan_lds_bytes)
-  constexpr size_t TAILB = sizeof(ScLostLds<GW>) > sizeof(ScFcLds) ? sizeof(ScLostLds<GW>) : sizeof(ScFcLds);
-  int32_t* Lra = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) +
-                                            SC_WAVES * TAILB) + wave * SC_FC_RING * 64;
   const int RS = R | 1;
   if constexpr (TAB) {
     for (int i = threadIdx.x; i < R * GW; i += blockDim.x) {
@@ -497,8 +507,7 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
       tV = ((double)qi * c.skw[skj[0]]) * c.inV[i];
     }
     inv[0] = iv;
-#pragma unroll
-    for (int q = 0; q < SC_FC_RING; q++) Lra[q * 64 + lane] = ring_a[q];  // (for phase C)
+
     // inbound cost (reward_calculator.py:144-151): fixed and variable terms summed over SKUs in order
     Lw->dscr[lane] = tF;
     wave_sync();
@@ -962,7 +971,7 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
         hv[a] = a < n_hist ? s.hist[((int64_t)(q < 0 ? q + MSC_HISTORY : q) * WK + i) * E + e] : 0;
       }
 #pragma unroll
-      for (int q = 0; q < SC_FC_RING; q++) rv[q] = FA ? Lra[q * 64 + lane] : (q < RING ? s.ring_q[((int64_t)i * RING + q) * E + e] : 0);
+      for (int q = 0; q < SC_FC_RING; q++) rv[q] = q < RING ? s.ring_q[((int64_t)i * RING + q) * E + e] : 0;
     }
     const int dh = home_done ? inc_h[0] : 0;  // this step's incoming home demand (step_a zeroed s.inc)
     const int sh = home_done ? shh_h[0] : 0, sa = (inv0[0] - inv[0]) - sh;
@@ -990,13 +999,8 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
     Lf->v[FC_SH][lane] = sh;
     Lf->v[FC_SA][lane] = sa;
     Lf->v[FC_PEND][lane] = pend;
-    Lf->v[FC_ELT][lane] = eltv;
     Lf->v[FC_FC][lane] = __float_as_int(fcn);
     Lf->v[FC_RM][lane] = __float_as_int(rm);
-#pragma unroll
-    for (int q = 0; q < SC_FC_RING; q++) Lf->v[FC_RING + q][lane] = rv[q];
-#pragma unroll
-    for (int a = 0; a < MSC_HISTORY; a++) Lf->v[FC_HIST + a][lane] = hv[a];
     Lw->dscr[lane] = hterm;
     wave_sync();
     const bool agent = sg == 0 && w < W;  // lane w builds agent w
@@ -1029,7 +1033,7 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
     // the observation, every lane (s, w) writing SKU s's values of agent w (obs_emit's arithmetic
     // value by value; the agent's totals from the staged SKU values, in SKU order)
     float* dst = trunc ? io.final_obs : io.obs;
-    if (dst && lv) fc_obs_lane<K, GW>(c, Lf, w, sk0, tm, n_hist, dst + (e * W + w) * (int64_t)c.L);
+    if (dst && lv) fc_obs_lane<K, GW>(c, Lf, w, sk0, tm, n_hist, eltv, rv, hv, dst + (e * W + w) * (int64_t)c.L);
     // truncation: reset the env (one sequential RNG pass), then every agent's reset observation
     if (trunc) {
       if (lane == 0) reset_env<K>(c, s, e, 0, nullptr);
@@ -1044,7 +1048,7 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
   }
 }
 
-static bool alloc_scan_tab(const EnvConst& c, int GW) { return sc_tab_bytes(c.R, GW) <= SC_TAB_MAX; }
+static bool alloc_scan_tab(const EnvConst& c, int GW) { return c.sc_tab && sc_tab_bytes(c.R, GW) <= SC_TAB_MAX; }
 size_t alloc_scan_lds_bytes(const EnvConst& c) {
   const int GW = sc_gw(c.W), NS = sc_ns(c.K, GW);
   const size_t wave_b = NS > 1 ? sizeof(ScWaveLds<2>) : sizeof(ScWaveLds<1>);
@@ -1052,7 +1056,7 @@ size_t alloc_scan_lds_bytes(const EnvConst& c) {
   // (the fused phase C stages its inputs where the deferred regions were)
   const size_t tail_b = c.fuse_c ? (lost_b > sizeof(ScFcLds) ? lost_b : sizeof(ScFcLds)) : (c.scan_defer ? lost_b : 0);
   return (alloc_scan_tab(c, GW) ? sc_tab_bytes(c.R, GW) : 0) + sizeof(int32_t) * ((c.R + 3) & ~3) +
-         SC_WAVES * wave_b + SC_WAVES * tail_b + (c.fuse_a ? (size_t)SC_WAVES * SC_FC_RING * 64 * sizeof(int32_t) : 0);
+         SC_WAVES * wave_b + SC_WAVES * tail_b;
 }
 // phase C fused into the scan allocator: one slot per lane (<= 8 warehouses), pending rings of at
 // most SC_FC_RING slots

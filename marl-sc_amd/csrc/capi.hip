@@ -482,6 +482,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     // phase A too when it has no per-env RNG work (fixed lead times; Poisson demand: the empirical
     // sampler draws its window start in phase A). MSC_FUSE_A=0 keeps the step_a kernel.
     c.fuse_a = c.alloc_impl == 2 && c.fuse_c && d->lead_type != MSC_LEAD_STOCHASTIC && d->demand_type == MSC_DEMAND_POISSON ? 1 : 0;
+    c.sc_tab = 1;
+    if (const char* st = getenv("MSC_SC_TAB")) c.sc_tab = atoi(st) != 0 ? 1 : 0;
     c.sb_gw = 0;
     if (const char* g = getenv("MSC_SB_GW")) {
       const int v = atoi(g);
@@ -728,8 +730,13 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       env->ea_enabled = true;
       env->obs_stage_pe = c.obs_stage;
       env->chain_prio_pe = c.chain_prio;
-      // refill batch: a batch freed by episodes n-B+1 .. n is needed S-B episodes later
-      int B = S / 4 > 1 ? S / 4 : 1;
+      // refill batch: a batch freed by episodes n-B+1 .. n is needed S-B episodes later. A generation
+      // chunk's duration is one lane's parse chain whatever the slots per launch, so the slots per
+      // launch set the generation rate: at 4,096 envs 4 per launch (16,384 lanes) could not keep up
+      // with the step (C2 sustained 173 M agent-steps/s over 96 episodes), 8 per launch can (207 M,
+      // profiles/r05/ab_ea_batch.txt); at 32,768 envs a single slot per launch already fills the chip
+      int B = E <= 8192 ? S / 2 : S / 4;
+      B = B > 1 ? B : 1;
       if (const char* eb = getenv("MSC_EA_BATCH")) B = atoi(eb);
       env->ea_batch = B < 1 ? 1 : (B > S - 1 ? S - 1 : B);
       // step_c's observation staging (up to 80 KB of LDS per block) stalls behind a generation
