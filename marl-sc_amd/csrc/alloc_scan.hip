@@ -411,8 +411,13 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
   double2* Ltab = reinterpret_cast<double2*>(sc_lds);  // [w][R | 1] {of, ov}
   int32_t* Lcl = reinterpret_cast<int32_t*>(sc_lds + (TAB ? sc_tab_bytes(R, GW) : 0));  // [R] closest warehouse
   ScWaveLds<NS>* Lw = reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + wave;
-  ScLostLds<GW>* Ll =
-      reinterpret_cast<ScLostLds<GW>*>(reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) + wave;
+  // per-wave tail: the deferred lost-sales regions, aliased by the fused phase C's staging (the stride
+  // is the larger of the two, as alloc_scan_lds_bytes sizes it)
+  constexpr size_t TAILB =
+      FC && sizeof(ScFcLds) > sizeof(ScLostLds<GW>) ? sizeof(ScFcLds) : sizeof(ScLostLds<GW>);
+  static_assert(TAILB % 16 == 0, "per-wave tail keeps 16-byte alignment");
+  ScLostLds<GW>* Ll = reinterpret_cast<ScLostLds<GW>*>(
+      reinterpret_cast<char*>(reinterpret_cast<ScWaveLds<NS>*>(Lcl + ((R + 3) & ~3)) + SC_WAVES) + wave * TAILB);
   constexpr int LA = ScLostLds<GW>::LA;
   const int RS = R | 1;
   if constexpr (TAB) {
