@@ -176,6 +176,11 @@ def window_work(w0: dict, w1: dict, n_envs: int, steps: int) -> dict:
     ea_l = int(w1["ea_launches"] - w0["ea_launches"])
     ea_w = int(round(w1["ea_env_steps"] - w0["ea_env_steps"]))
     dl = int(w1["demand_launches"] - w0["demand_launches"])
+    if ea_l == 0 and dl == 0:
+        # empirical demand: the trace is resident in HBM and the step reads it directly (no generation)
+        return {"ea_launches_in_window": 0, "demand_launches_in_window": 0,
+                "env_steps_timed": int(n_envs) * int(steps), "steps_in_window": int(w1["steps"] - w0["steps"]),
+                "ahead_change_steps": None, "demand": "trace resident in HBM, no generation work"}
     return {"ea_launches_in_window": ea_l, "ea_env_steps_in_window": ea_w, "demand_launches_in_window": dl,
             "demand_env_steps_in_window": ea_w + dl * n_envs, "env_steps_timed": int(n_envs) * int(steps),
             "steps_in_window": int(w1["steps"] - w0["steps"]),

@@ -494,15 +494,18 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       // step_b's block tables ({of, ov} rows [2][R][W] f64 + closest [R] i32) in LDS: when small
       // (16 KB, room for the blocks of the pipelined demand kernel beside the step), or, with
       // empirical demand (no demand kernel beside the step), when the step_b blocks one CU holds at
-      // this env count fit its 160 KB with them (C5, 8,192 envs x 16 warehouses: 2 blocks of 16 KB of
-      // record windows + 65 KB of tables); otherwise each region change reads its cost row from L2
+      // this env count fit its 160 KB with them (C5, 8,192 envs x 16 warehouses: one 8-wave block per
+      // CU, 32 KB of record windows + 66.5 KB of tables); otherwise each region change reads its cost
+      // row from L2, and its wait also drains the record windows' LDS-DMA and the stores in flight
       int ncu = 256;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
       int gw = W <= 2 ? 2 : W <= 4 ? 4 : W <= 8 ? 8 : W <= 16 ? 16 : 32;
       if (const char* g = getenv("MSC_SB_GW")) gw = atoi(g) > gw && atoi(g) <= 32 ? atoi(g) : gw;
-      const int64_t blocks = (n_envs * gw + 255) / 256, per_cu = (blocks + ncu - 1) / ncu;
+      // (blocks of 8 waves for 16- and 32-lane groups with the tables, else 4: step_b_waves)
+      const int bw = gw >= 16 ? 8 : 4;
+      const int64_t blocks = (n_envs * gw + 64 * bw - 1) / (64 * bw), per_cu = (blocks + ncu - 1) / ncu;
       const size_t tab = (size_t)2 * R * W * sizeof(double) + (size_t)R * sizeof(int32_t);
-      const size_t blk = (size_t)4 * 2 * 128 * 16 + tab;  // 4 waves x 2 windows x SB_REC records + tables
+      const size_t blk = (size_t)bw * 2 * 128 * 16 + tab;  // waves x 2 windows x SB_REC records + tables
       c.sb_tab = tab <= 16 * 1024 ? 1
                : (d->demand_type == MSC_DEMAND_EMPIRICAL && blk <= 160 * 1024 && (int64_t)blk * per_cu <= 160 * 1024) ? 1 : 0;
       if (const char* st = getenv("MSC_SB_TAB")) c.sb_tab = atoi(st) != 0 && blk <= 160 * 1024 ? 1 : 0;

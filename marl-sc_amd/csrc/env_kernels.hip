@@ -984,8 +984,12 @@ __host__ __device__ constexpr int step_b_chunk(int GW, int NV) { return SB_REC /
 __host__ __device__ constexpr size_t step_b_tab_bytes(int R, int W) {
   return (size_t)2 * R * W * sizeof(double) + (size_t)R * sizeof(int32_t);
 }
-__host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab) {
-  return (size_t)4 * 2 * SB_REC * 16 + (tab ? step_b_tab_bytes(R, W) : 0);
+// waves per block: 8 for 16- and 32-lane groups with the tables in LDS (C5: one block per CU holds
+// the 66.5-KB table once for 8 waves' record windows; two 4-wave blocks per CU would need it twice),
+// else 4
+__host__ __device__ constexpr int step_b_waves(int GW, bool tab) { return GW >= 16 && tab ? 8 : 4; }
+__host__ __device__ constexpr size_t step_b_lds_bytes(int R, int W, bool tab, int waves) {
+  return (size_t)waves * 2 * SB_REC * 16 + (tab ? step_b_tab_bytes(R, W) : 0);
 }
 
 // (group_np_sum: kcommon.hpp)
@@ -1169,13 +1173,17 @@ __device__ __forceinline__ void step_b_phase_c(const EnvConst& c, const EnvState
 
 // (above 8 SKUs the K-wide register arrays of a lane need the larger budget of 2 waves per SIMD)
 template <int K, int GW, bool DBG, bool TAB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : GW >= 16 ? MSC_SB_WPE16 : MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+__global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 : GW >= 16 ? MSC_SB_WPE16 : MSC_SB_WPE))) void step_b_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   const EnvConst& c = dp->c;
   const EnvState& s = dp->s;
   const int W = c.W, WK = W * K, R = c.R;
   const int64_t E = c.E;
   const int w = threadIdx.x % GW;
-  const int64_t eg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / GW;
+  // visiting slot of this lane group: wave k of block b runs slot-wave k * gridDim.x + b, so with the
+  // envs sorted by order count a block (one CU at C5) holds waves from the whole range of loads
+  // instead of 8 consecutive ones -- the busiest envs' waves no longer share their CU's SIMDs only
+  // with each other -- while a wave still holds consecutive (similar) envs
+  const int64_t eg = ((int64_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x) * (64 / GW) + (threadIdx.x & 63) / GW;
   const int64_t e = (c.alloc_sort && eg < E) ? (int64_t)s.perm[eg] : eg;
   const bool ev = e < E, wl = w < W;
   const msc_step_info info = io.info;
@@ -1190,7 +1198,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
   if (MSC_SB_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SB_PRIO);
   uint4* win = sb_lds + wave * 2 * SB_REC;  // this wave's two windows [2][CH][NVR][EPW]
   const MSC_GLOBAL int32_t* closest = gp(c.closest);
-  double* lof = TAB ? reinterpret_cast<double*>(sb_lds + 4 * 2 * SB_REC) : nullptr;
+  double* lof = TAB ? reinterpret_cast<double*>(sb_lds + step_b_waves(GW, TAB) * 2 * SB_REC) : nullptr;
   double* lov = TAB ? lof + R * W : nullptr;
   int32_t* lcl = TAB ? reinterpret_cast<int32_t*>(lov + R * W) : nullptr;
   if constexpr (TAB) {
@@ -1234,6 +1242,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     const int v = __shfl_xor(wmax, o);
     wmax = v > wmax ? v : wmax;
   }
+  // this warehouse's home region (argmin over regions of its distance row, multi_env.py:144)
+  int myhome = wl ? c.home_of[w] : -1;
+  // the loaded values the order loop reads, settled before the first window's LDS-DMA: the
+  // compiler's wait for a load first used inside the loop is a vmcnt(0) there, which would also
+  // wait for the record windows in flight
+  myhome = vsettle(myhome);
+#pragma unroll
+  for (int sk = 0; sk < K; sk++) inv[sk] = vsettle(inv[sk]);
   auto issue = [&](int chunk) {  // LDS-DMA of window `chunk` into buffer chunk % 2
     uint4* dst = win + (chunk & 1) * SB_REC;
 #pragma unroll
@@ -1271,8 +1287,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
     skw[sk] = sgpr_d(c.skw[sk]);
     penk[sk] = sgpr_d(pps ? c.pen[sk] : c.pen_scalar);
   }
-  // this warehouse's home region (argmin over regions of its distance row, multi_env.py:144)
-  const int myhome = wl ? c.home_of[w] : -1;
   int cur = -1, lost_cnt = 0;
   bool home_done = false;
   int u[K], dsum[K];
@@ -1353,7 +1367,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    if (oi > n_orders) continue;  // this env is done (lanes of busier envs go on)
+    // Predicated form: one pass per order index for every lane of the wave, no lane-divergent
+    // `continue` or `break` (each costs the wave an exec-mask save / branch / restore at every order,
+    // whether or not a lane diverges): a lane whose env has no order at oi carries rem = 0, key ~0.
+    const bool live = oi <= n_orders;  // this env's orders, then its last region's epilogue at oi == n
+    const bool rec = oi < n_orders;
     int r = -1;
     int d[K];
     {
@@ -1363,17 +1381,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       } ur;
 #pragma unroll
       for (int j = 0; j < NVR; j++) ur.v[j] = win[((oi / CH) & 1) * SB_REC + ((oi % CH) * NVR + j) * EPW + myjj];
-      if (oi < n_orders) r = ur.h[0];
+      if (rec) r = ur.h[0];
 #pragma unroll
-      for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
+      for (int sk = 0; sk < K; sk++) d[sk] = rec ? (int)ur.h[1 + sk] : 0;
     }
     // (prof build: the time of this block and its passes counted for the whole wave, i.e. also when
     // only another env of the wave changes region)
     PROF_T(q_f0);
 #ifdef MSC_PROF
-    PROF_ADD(q_nfin, __ballot(r != cur) != 0 ? 1ull : 0ull);
+    PROF_ADD(q_nfin, __ballot(live && r != cur) != 0 ? 1ull : 0ull);
 #endif
-    if (r != cur) {
+    if (live && r != cur) {
       if (cur >= 0) finalize(cur);
       if (r >= 0 && wl) {
         cof = cost_of(r);
@@ -1385,34 +1403,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
     }
     PROF_ADD(q_fin, PROF_NOW() - q_f0);
-    if (oi == n_orders) continue;
     bool any_d = false;
-    double tw = 0.0;
+    // (the weight sum starts at its first product: 0.0 + x == x for the products here, which are
+    // never -0.0 -- quantities >= 0 times PositiveFloat weights, schema.py:174)
+    double tw = (double)d[0] * skw[0];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       dsum[sk] += d[sk];
       any_d |= d[sk] > 0;
-      tw += (double)d[sk] * skw[sk];
+      if (sk > 0) tw += (double)d[sk] * skw[sk];
     }
-    if (!any_d) continue;  // an empty order ships nothing and is never lost
+    // (an empty order ships nothing and is never lost; d is 0 past the env's orders)
+    const bool ord = any_d;
     int rem[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
+    unsigned dpk[NP];  // the order's quantities packed like the winners' fills
+#pragma unroll
+    for (int j = 0; j < NP; j++) dpk[j] = (unsigned)d[2 * j] | (2 * j + 1 < K ? (unsigned)d[2 * j + 1] << 16 : 0u);
     const double mycost = cof + cov * tw;  // demand_allocator.py:168-172
     // total-order key of the cost (negatives and -0.0 included), so the group min is an integer min
     const uint64_t cbits = (uint64_t)__double_as_longlong(mycost + 0.0);
     const uint64_t ckey = cbits ^ ((uint64_t)((int64_t)cbits >> 63) | 0x8000000000000000ull);
     int used = 0;
-    bool open = true;
+    bool open = ord;
     PROF_T(q_a0);
-    while (open) {
+    // allocation rounds while any group of the wave has its order open (a wave-uniform loop; the
+    // groups whose order closed go through the remaining rounds with key ~0 and no fills)
+    while (__ballot(open) != 0ull) {
       PROF_ADD(q_iter, 1);
       // a warehouse that shipped already has nothing left that the order still needs
       // (fill = min(rem, inv) zeroes one of the two for every SKU), so "has" alone excludes it
       bool has = false;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) has |= rem[sk] > 0 && inv[sk] > 0;
-      const uint64_t key = (has && wl) ? ckey : ~0ull;
+      const uint64_t key = (open && has && wl) ? ckey : ~0ull;
       uint64_t mk = key;
       {
         auto step = [&](uint64_t o) { mk = o < mk ? o : mk; };
@@ -1426,11 +1451,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
         if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
         if constexpr (GW >= 32) step(dpp64([](int v) { return dpp_x<4>(v); }, mk));
       }
-      if (mk == ~0ull) break;  // nobody holds a still-needed SKU
+      const bool go = mk != ~0ull;  // (group-uniform) somebody holds a still-needed SKU: a fill
       // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
       const uint64_t tie = __ballot(key == mk);
       const int bw = __builtin_ctzll(tie >> gbase);
-      const bool me = w == bw;
+      const bool me = go && w == bw;
       int fl[K];
 #pragma unroll
       for (int sk = 0; sk < K; sk++) fl[sk] = me ? (rem[sk] < inv[sk] ? rem[sk] : inv[sk]) : 0;
@@ -1446,41 +1471,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       {
         const int src = (gbase + bw) << 2;
 #pragma unroll
-        for (int j = 0; j < NP; j++) pk[j] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)pk[j]);
+        for (int j = 0; j < NP; j++) pk[j] = go ? (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)pk[j]) : 0u;
       }
 #else
 #pragma unroll
       for (int j = 0; j < NP; j++) pk[j] = (unsigned)group_reduce<GW>((int)pk[j], [](int a, int b) { return a | b; });
 #endif
       bool done = true;
+      int fsum = 0;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) {
         rem[sk] -= (int)((pk[sk >> 1] >> (16 * (sk & 1))) & 0xffffu);
         done &= rem[sk] <= 0;
+        inv[sk] -= fl[sk];  // (fl is 0 off the winner lane)
+        qsr[sk] += fl[sk];
+        fsum += fl[sk];
       }
-      if (me) {
-        double fw = 0.0;
-        int fsum = 0;
+      bool whole = true;  // the fills are the whole order: their weight is tw, computed the same way
+#pragma unroll
+      for (int j = 0; j < NP; j++) whole &= pk[j] == dpk[j];
+      double cst = mycost;
+      if (__ballot(me && !whole) != 0ull) {  // (wave-uniform) a partial fill: its own weight and cost
+        double fw = (double)fl[0] * skw[0];
+#pragma unroll
+        for (int sk = 1; sk < K; sk++) fw += (double)fl[sk] * skw[sk];
+        cst = (whole || fw == tw) ? mycost : cof + cov * fw;  // whole order from here: the ranking cost bit for bit
+      }
+      out += me ? cst : 0.0;  // (out >= +0.0: adding +0.0 leaves it unchanged)
+      if (dbg && me) {
 #pragma unroll
         for (int sk = 0; sk < K; sk++) {
-          inv[sk] -= fl[sk];
-          qsr[sk] += fl[sk];
-          fsum += fl[sk];
-          fw += (double)fl[sk] * skw[sk];
+          if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] += fl[sk];
+          if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
         }
-        out += fw == tw ? mycost : cof + cov * fw;  // whole order from here: the ranking cost bit for bit
-        if (dbg) {
-#pragma unroll
-          for (int sk = 0; sk < K; sk++) {
-            if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] += fl[sk];
-            if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
-          }
-          if (info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] += 1;
-          if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] += fsum;
-        }
+        if (info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] += 1;
+        if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] += fsum;
       }
-      used++;
-      open = !done && used < maxwh;
+      used += go ? 1 : 0;
+      open = open && go && !done && used < maxwh;
     }
     PROF_ADD(q_alloc, PROF_NOW() - q_a0);
     bool anyrem = false;
@@ -1489,7 +1517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? 2 :
       anyrem |= rem[sk] > 0;
       u[sk] += rem[sk] > 0 ? rem[sk] : 0;
     }
-    lost_cnt += anyrem ? 1 : 0;
+    lost_cnt += anyrem ? 1 : 0;  // (rem is 0 unless this lane's env had a nonempty order at oi)
   }
   PROF_ADD(q_all, PROF_NOW() - q_t0);
   PROF_FLUSH(10, q_all);
@@ -1853,12 +1881,13 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     if (ea != hipSuccess) return ea;
   } else {
     if (c.alloc_sort) launch_alloc_sort(d, io, st);
-    const size_t lds_b = step_b_lds_bytes(c.R, c.W, tab);
+    const int bt = 64 * step_b_waves(GW, tab);
+    const size_t lds_b = step_b_lds_bytes(c.R, c.W, tab, bt / 64);
     if (lds_b > 64 * 1024) {
       const hipError_t e = hipFuncSetAttribute((const void*)b, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + 255) / 256)), dim3(256), lds_b, st, d, io);
+    hipLaunchKernelGGL(b, dim3((unsigned)((c.E * GW + bt - 1) / bt)), dim3(bt), lds_b, st, d, io);
   }
   if (c.fuse_c && c.alloc_impl != 0) return hipGetLastError();  // (phase C ran inside the allocator)
   const int stage_w = c.obs_stage ? (c.W + (c.obs_stage > 1 ? c.obs_stage : 1) - 1) / (c.obs_stage > 1 ? c.obs_stage : 1) : 0;

@@ -40,6 +40,14 @@ __device__ __forceinline__ double sgpr_d(double v) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// v as the output of an (empty) asm statement: no load of it is pending afterwards, so the compiler
+// places its wait for the load here instead of at the value's first use (inside a loop, that wait
+// is a vmcnt(0) that also drains every LDS-DMA and store in flight)
+__device__ __forceinline__ int vsettle(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // numpy pairwise sum (add.reduce, n <= 16): sequential below 8 elements, else 8 accumulators
 // (static indices only: v stays in registers)
 __device__ __forceinline__ double np_sum_f64_16(const double (&v)[16], int n) {
@@ -70,7 +78,9 @@ __device__ __forceinline__ int dpp_x(int v) {
     return __shfl_xor(v, 16);
   } else {
     constexpr int ctrl = S == 0 ? 0xB1 : S == 1 ? 0x4E : S == 2 ? 0x141 : 0x140;
-    return __builtin_amdgcn_update_dpp(0, v, ctrl, 0xF, 0xF, false);
+    // (every lane of these patterns has a source inside its row, so no `old` value is needed:
+    // mov_dpp with bound_ctrl leaves the compiler free to skip zeroing the destination first)
+    return __builtin_amdgcn_mov_dpp(v, ctrl, 0xF, 0xF, true);
   }
 }
 template <int S>

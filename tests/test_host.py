@@ -410,3 +410,19 @@ def test_group_mean_is_pandas_groupby_mean():
         want = pd.DataFrame({"k": 0, "v": v}).groupby("k")["v"].mean().iloc[0]
         got = _group_mean(v.tolist())
         assert (got == want) or (got != got and want != want), (v, got, want)
+
+
+def test_bench_window_accounting():
+    """bench.window_work: per-step demand, episode-ahead refills and a resident trace (no generation)."""
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    z = {"ea_launches": 0, "ea_env_steps": 0, "demand_launches": 0, "steps": 0}
+    per_step = bench.window_work(z, dict(z, demand_launches=10, steps=10), 64, 10)
+    assert per_step["demand_env_steps_in_window"] == 640 and per_step["ahead_change_steps"] == 0.0
+    ahead = bench.window_work(z, dict(z, ea_launches=2, ea_env_steps=64 * 100, steps=50), 64, 50)
+    assert ahead["ahead_change_steps"] == 50.0
+    drained = bench.window_work(z, dict(z, steps=50, ea_launches=1, ea_env_steps=64 * 20), 64, 50)
+    assert drained["ahead_change_steps"] == -30.0
+    trace = bench.window_work(z, dict(z, steps=7), 64, 7)
+    assert trace["ahead_change_steps"] is None and trace["env_steps_timed"] == 448
