@@ -1367,11 +1367,7 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    // Predicated form: one pass per order index for every lane of the wave, no lane-divergent
-    // `continue` or `break` (each costs the wave an exec-mask save / branch / restore at every order,
-    // whether or not a lane diverges): a lane whose env has no order at oi carries rem = 0, key ~0.
-    const bool live = oi <= n_orders;  // this env's orders, then its last region's epilogue at oi == n
-    const bool rec = oi < n_orders;
+    if (oi > n_orders) continue;  // this env is done (lanes of busier envs go on)
     int r = -1;
     int d[K];
     {
@@ -1381,17 +1377,17 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       } ur;
 #pragma unroll
       for (int j = 0; j < NVR; j++) ur.v[j] = win[((oi / CH) & 1) * SB_REC + ((oi % CH) * NVR + j) * EPW + myjj];
-      if (rec) r = ur.h[0];
+      if (oi < n_orders) r = ur.h[0];
 #pragma unroll
-      for (int sk = 0; sk < K; sk++) d[sk] = rec ? (int)ur.h[1 + sk] : 0;
+      for (int sk = 0; sk < K; sk++) d[sk] = ur.h[1 + sk];
     }
     // (prof build: the time of this block and its passes counted for the whole wave, i.e. also when
     // only another env of the wave changes region)
     PROF_T(q_f0);
 #ifdef MSC_PROF
-    PROF_ADD(q_nfin, __ballot(live && r != cur) != 0 ? 1ull : 0ull);
+    PROF_ADD(q_nfin, __ballot(r != cur) != 0 ? 1ull : 0ull);
 #endif
-    if (live && r != cur) {
+    if (r != cur) {
       if (cur >= 0) finalize(cur);
       if (r >= 0 && wl) {
         cof = cost_of(r);
@@ -1403,6 +1399,7 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
     }
     PROF_ADD(q_fin, PROF_NOW() - q_f0);
+    if (oi == n_orders) continue;
     bool any_d = false;
     // (the weight sum starts at its first product: 0.0 + x == x for the products here, which are
     // never -0.0 -- quantities >= 0 times PositiveFloat weights, schema.py:174)
@@ -1413,8 +1410,7 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       any_d |= d[sk] > 0;
       if (sk > 0) tw += (double)d[sk] * skw[sk];
     }
-    // (an empty order ships nothing and is never lost; d is 0 past the env's orders)
-    const bool ord = any_d;
+    if (!any_d) continue;  // an empty order ships nothing and is never lost
     int rem[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
@@ -1426,18 +1422,16 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
     const uint64_t cbits = (uint64_t)__double_as_longlong(mycost + 0.0);
     const uint64_t ckey = cbits ^ ((uint64_t)((int64_t)cbits >> 63) | 0x8000000000000000ull);
     int used = 0;
-    bool open = ord;
+    bool open = true;
     PROF_T(q_a0);
-    // allocation rounds while any group of the wave has its order open (a wave-uniform loop; the
-    // groups whose order closed go through the remaining rounds with key ~0 and no fills)
-    while (__ballot(open) != 0ull) {
+    while (open) {
       PROF_ADD(q_iter, 1);
       // a warehouse that shipped already has nothing left that the order still needs
       // (fill = min(rem, inv) zeroes one of the two for every SKU), so "has" alone excludes it
       bool has = false;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) has |= rem[sk] > 0 && inv[sk] > 0;
-      const uint64_t key = (open && has && wl) ? ckey : ~0ull;
+      const uint64_t key = (has && wl) ? ckey : ~0ull;
       uint64_t mk = key;
       {
         auto step = [&](uint64_t o) { mk = o < mk ? o : mk; };
@@ -1451,11 +1445,11 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
         if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
         if constexpr (GW >= 32) step(dpp64([](int v) { return dpp_x<4>(v); }, mk));
       }
-      const bool go = mk != ~0ull;  // (group-uniform) somebody holds a still-needed SKU: a fill
+      if (mk == ~0ull) break;  // nobody holds a still-needed SKU
       // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
       const uint64_t tie = __ballot(key == mk);
       const int bw = __builtin_ctzll(tie >> gbase);
-      const bool me = go && w == bw;
+      const bool me = w == bw;
       int fl[K];
 #pragma unroll
       for (int sk = 0; sk < K; sk++) fl[sk] = me ? (rem[sk] < inv[sk] ? rem[sk] : inv[sk]) : 0;
@@ -1471,44 +1465,49 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       {
         const int src = (gbase + bw) << 2;
 #pragma unroll
-        for (int j = 0; j < NP; j++) pk[j] = go ? (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)pk[j]) : 0u;
+        for (int j = 0; j < NP; j++) pk[j] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)pk[j]);
       }
 #else
 #pragma unroll
       for (int j = 0; j < NP; j++) pk[j] = (unsigned)group_reduce<GW>((int)pk[j], [](int a, int b) { return a | b; });
 #endif
       bool done = true;
-      int fsum = 0;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) {
         rem[sk] -= (int)((pk[sk >> 1] >> (16 * (sk & 1))) & 0xffffu);
         done &= rem[sk] <= 0;
-        inv[sk] -= fl[sk];  // (fl is 0 off the winner lane)
-        qsr[sk] += fl[sk];
-        fsum += fl[sk];
       }
-      bool whole = true;  // the fills are the whole order: their weight is tw, computed the same way
-#pragma unroll
-      for (int j = 0; j < NP; j++) whole &= pk[j] == dpk[j];
-      double cst = mycost;
-      if (__ballot(me && !whole) != 0ull) {  // (wave-uniform) a partial fill: its own weight and cost
-        double fw = (double)fl[0] * skw[0];
-#pragma unroll
-        for (int sk = 1; sk < K; sk++) fw += (double)fl[sk] * skw[sk];
-        cst = (whole || fw == tw) ? mycost : cof + cov * fw;  // whole order from here: the ranking cost bit for bit
-      }
-      out += me ? cst : 0.0;  // (out >= +0.0: adding +0.0 leaves it unchanged)
-      if (dbg && me) {
+      if (me) {
+        int fsum = 0;
 #pragma unroll
         for (int sk = 0; sk < K; sk++) {
-          if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] += fl[sk];
-          if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
+          inv[sk] -= fl[sk];
+          qsr[sk] += fl[sk];
+          fsum += fl[sk];
         }
-        if (info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] += 1;
-        if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] += fsum;
+        bool whole = true;  // the fills are the whole order: their weight is tw, computed the same way
+#pragma unroll
+        for (int j = 0; j < NP; j++) whole &= pk[j] == dpk[j];
+        if (whole) {
+          out += mycost;
+        } else {
+          double fw = (double)fl[0] * skw[0];
+#pragma unroll
+          for (int sk = 1; sk < K; sk++) fw += (double)fl[sk] * skw[sk];
+          out += fw == tw ? mycost : cof + cov * fw;  // whole order from here: the ranking cost bit for bit
+        }
+        if (dbg) {
+#pragma unroll
+          for (int sk = 0; sk < K; sk++) {
+            if (info.shipment_quantities_by_sku) info.shipment_quantities_by_sku[((e * W + w) * R + r) * K + sk] += fl[sk];
+            if (info.fulfilled_per_warehouse) info.fulfilled_per_warehouse[e * WK + w * K + sk] += fl[sk];
+          }
+          if (info.shipment_counts) info.shipment_counts[(e * W + w) * R + r] += 1;
+          if (info.shipment_quantities) info.shipment_quantities[(e * W + w) * R + r] += fsum;
+        }
       }
-      used += go ? 1 : 0;
-      open = open && go && !done && used < maxwh;
+      used++;
+      open = !done && used < maxwh;
     }
     PROF_ADD(q_alloc, PROF_NOW() - q_a0);
     bool anyrem = false;
@@ -1517,7 +1516,7 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       anyrem |= rem[sk] > 0;
       u[sk] += rem[sk] > 0 ? rem[sk] : 0;
     }
-    lost_cnt += anyrem ? 1 : 0;  // (rem is 0 unless this lane's env had a nonempty order at oi)
+    lost_cnt += anyrem ? 1 : 0;
   }
   PROF_ADD(q_all, PROF_NOW() - q_t0);
   PROF_FLUSH(10, q_all);
