@@ -356,7 +356,12 @@ def c5_line(args, rank: int):
             out["roofline"] = issue_object(
                 sum(cn), tm["step_ms"] * 1e-3, None, kernel="step_kernels (" + " + ".join(names) + ")",
                 insts_per_step=int(sum(cn)), traffic=sum(tb) if all(x is not None for x in tb) else None,
-                note="the allocation is one env per lane group on the per-order argmin chain (DESIGN.md section 3)")
+                note="one env per 16-lane group (4 envs per wave, 2 waves per SIMD at 8,192 envs): the per-order "
+                     "chain's whole instruction stream (VALU + SALU, SQ_INSTS_SALU in the PMC summary) at one wave's "
+                     "issue cadence bounds it, not the VALU peak; phase C runs inside step_b (DESIGN.md section 3)")
+            salu = [cs[n].get("SQ_INSTS_SALU") for n in names]
+            if all(x is not None for x in salu):
+                out["roofline"]["salu_insts_per_step"] = int(sum(salu))
     return out
 
 
