@@ -417,7 +417,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     // (demand_ab_kernel: measured slower), "park4" the round-1 parser
     c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : impl && strcmp(impl, "ab") == 0 ? 7 : 0;
     const char* gen = getenv("MSC_DEMAND_GEN");
-    c.demand_gen = gen && atoi(gen) >= 1 && atoi(gen) <= 3 ? atoi(gen) : 3;
+    // (5 and 7: A/B instantiations for 5 SKUs only, more generator waves per 64 envs)
+    c.demand_gen = gen && ((atoi(gen) >= 1 && atoi(gen) <= 3) || (K == 5 && (atoi(gen) == 5 || atoi(gen) == 7))) ? atoi(gen) : 3;
     const char* v = getenv("MSC_DEMAND_EPW");
     const int x = v ? atoi(v) : 64;
     c.epw_dem = x == 16 || x == 32 || x == 64 ? x : 64;

@@ -31,7 +31,7 @@ struct EnvConst {
   int32_t action_type, lead_type, dev_per_sku, lost_type, scope, norm, wid, num_eval, max_wh;
   int32_t demand_type, init_type, init_min, init_max, hold_per_sku, pen_per_sku, tr_rows;
   int32_t demand_impl;  // 0 = generator waves + unit-per-round parser (default); 5 = park4 (A/B)
-  int32_t demand_gen;   // generator waves per block of the split demand kernel (1, 2 or 3)
+  int32_t demand_gen;   // generator waves per block of the split demand kernel (1, 2 or 3; 5 / 7 A/B at 5 SKUs)
   int32_t park_min;     // parked lanes that trigger a settle pass of the demand parser (MSC_PARK_MIN)
   int32_t parser_rot;   // which wave of a demand block parses: (wave + rot(block)) % (1 + G) == 0 (A/B knob)
   int32_t obs_stage;    // 1: step_c stages each wave's observations in LDS and writes them coalesced

@@ -1810,6 +1810,10 @@ static hipError_t launch_demand_k(const EnvConst& c, const DevEnv* d, hipStream_
   } else if (c.demand_gen == 2) {
     return launch_split_demand<K, 2>(c, d, st, ea);
   } else {
+    if constexpr (K == 5) {  // (A/B: 5 and 7 generator waves per block, 5 SKUs only)
+      if (c.demand_gen == 5) return launch_split_demand<K, 5>(c, d, st, ea);
+      if (c.demand_gen == 7) return launch_split_demand<K, 7>(c, d, st, ea);
+    }
     return launch_split_demand<K, 3>(c, d, st, ea);
   }
 }

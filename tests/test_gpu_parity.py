@@ -154,6 +154,18 @@ def test_bench_config_vs_oracle_across_episode_boundary():
     _lockstep(spec, 512, 110, check_every=10)
 
 
+@pytest.mark.parametrize("gen,ea", [(1, "0"), (2, "0"), (5, "0"), (7, "0"), (5, "1"), (7, "1")])
+def test_demand_generator_waves_vs_oracle(monkeypatch, gen, ea):
+    # the Poisson demand kernel with 1 / 2 / 5 / 7 generator waves per 64 envs (MSC_DEMAND_GEN; every
+    # other test runs the default 3), per step and episode-ahead, in lockstep with the oracle at the
+    # BASELINE 8 x 64 x 5 shape across an episode boundary (5 and 7: A/B instantiations at 5 SKUs)
+    monkeypatch.setenv("MSC_DEMAND_GEN", str(gen))
+    monkeypatch.setenv("MSC_EA", ea)
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=20)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 192, 45, seed=gen, check_every=5)
+
+
 @pytest.mark.usefixtures("alloc_impl_lpe")
 def test_c5_shape_vs_oracle():
     cfg = make_synthetic_env_config(16, 256, 5, episode_length=12)
