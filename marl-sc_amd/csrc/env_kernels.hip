@@ -1358,8 +1358,10 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
   PROF_DECL(q_iter);
   PROF_DECL(q_nfin);
   PROF_T(q_t0);
+  int wdue = CH;  // (wave-uniform) the next order index that opens a window
   for (int oi = 0; oi <= wmax; oi++) {
-    if (oi > 0 && oi % CH == 0) {  // wave-uniform: window oi / CH is due, start the one after
+    if (oi == wdue) {  // wave-uniform: window oi / CH is due, start the one after
+      wdue += CH;
       if (oi + CH <= wmax) {
         issue(oi / CH + 1);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPL) : "memory");
@@ -1400,17 +1402,16 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
     }
     PROF_ADD(q_fin, PROF_NOW() - q_f0);
     if (oi == n_orders) continue;
-    bool any_d = false;
     // (the weight sum starts at its first product: 0.0 + x == x for the products here, which are
     // never -0.0 -- quantities >= 0 times PositiveFloat weights, schema.py:174)
     double tw = (double)d[0] * skw[0];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       dsum[sk] += d[sk];
-      any_d |= d[sk] > 0;
       if (sk > 0) tw += (double)d[sk] * skw[sk];
     }
-    if (!any_d) continue;  // an empty order ships nothing and is never lost
+    // (an empty order needs no test of its own: no warehouse holds a needed SKU, so its first round
+    // ends the loop, and with nothing unfulfilled it is never lost)
     int rem[K];
 #pragma unroll
     for (int sk = 0; sk < K; sk++) rem[sk] = d[sk];
