@@ -1242,6 +1242,9 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
     const int v = __shfl_xor(wmax, o);
     wmax = v > wmax ? v : wmax;
   }
+  // (uniform after the butterfly; as a scalar, the order loop's exit and window tests are scalar
+  // compares instead of lane masks merged at every order)
+  wmax = __builtin_amdgcn_readfirstlane(wmax);
   // this warehouse's home region (argmin over regions of its distance row, multi_env.py:144)
   int myhome = wl ? c.home_of[w] : -1;
   // the loaded values the order loop reads, settled before the first window's LDS-DMA: the
@@ -1288,7 +1291,8 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
     penk[sk] = sgpr_d(pps ? c.pen[sk] : c.pen_scalar);
   }
   int cur = -1, lost_cnt = 0;
-  bool home_done = false;
+  int home_done = 0;  // (an int, not a bool: a lane-varying bool lives in a lane mask that every
+                     // exit of the order loop's branches merges again)
   int u[K], dsum[K];
 #pragma unroll
   for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
@@ -1336,7 +1340,7 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
         s.inc[(int64_t)(w * K + sk) * E + e] = dsum[sk];
         s.sc_shh[(int64_t)(w * K + sk) * E + e] = qsr[sk];
       }
-      home_done = true;
+      home_done = 1;
     }
     if (dbg && w == 0) {
 #pragma unroll
@@ -1528,7 +1532,7 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
   PROF_FLUSH(15, 1ull);
   if constexpr (K <= 8) {
     if (c.fuse_c) {  // (uniform) phase C here: the step_c kernel is not launched
-      step_b_phase_c<K, GW>(c, s, io, e, w, ev, wl, gbase, home_done, inv, pen, out);
+      step_b_phase_c<K, GW>(c, s, io, e, w, ev, wl, gbase, home_done != 0, inv, pen, out);
       return;
     }
   }
