@@ -1450,7 +1450,9 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
         if constexpr (GW >= 16) step(dpp64([](int v) { return dpp_x<3>(v); }, mk));
         if constexpr (GW >= 32) step(dpp64([](int v) { return dpp_x<4>(v); }, mk));
       }
-      if (mk == ~0ull) break;  // nobody holds a still-needed SKU
+      if (mk == ~0ull) {  // nobody holds a still-needed SKU: the order closes (an if/else, not a
+        open = false;     // break: one loop exit, no lane masks merged from a second one per round)
+      } else {
       // lowest warehouse among the group's minimum-cost lanes (argsort order on ties)
       const uint64_t tie = __ballot(key == mk);
       const int bw = __builtin_ctzll(tie >> gbase);
@@ -1513,6 +1515,7 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       }
       used++;
       open = !done && used < maxwh;
+      }
     }
     PROF_ADD(q_alloc, PROF_NOW() - q_a0);
     bool anyrem = false;
