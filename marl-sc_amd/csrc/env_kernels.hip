@@ -1518,13 +1518,15 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       }
     }
     PROF_ADD(q_alloc, PROF_NOW() - q_a0);
-    bool anyrem = false;
+    // (rem >= 0 throughout: every fill is min(rem, inv) with inv >= 0, so the unfulfilled units are
+    // rem itself and "any left" is an OR of the words)
+    int remor = 0;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
-      anyrem |= rem[sk] > 0;
-      u[sk] += rem[sk] > 0 ? rem[sk] : 0;
+      remor |= rem[sk];
+      u[sk] += rem[sk];
     }
-    lost_cnt += anyrem ? 1 : 0;
+    lost_cnt += remor != 0 ? 1 : 0;
   }
   PROF_ADD(q_all, PROF_NOW() - q_t0);
   PROF_FLUSH(10, q_all);
