@@ -1373,7 +1373,9 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    if (oi > n_orders) continue;  // this env is done (lanes of busier envs go on)
+    // (structured ifs, not `continue`: every exit of the body is a latch whose lane masks the loop
+    // merges at each order)
+    if (oi <= n_orders) {  // else this env is done (lanes of busier envs go on)
     int r = -1;
     int d[K];
     {
@@ -1405,7 +1407,7 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       for (int sk = 0; sk < K; sk++) u[sk] = dsum[sk] = 0;
     }
     PROF_ADD(q_fin, PROF_NOW() - q_f0);
-    if (oi == n_orders) continue;
+    if (oi < n_orders) {  // (at oi == n_orders only the last region's epilogue above)
     // (the weight sum starts at its first product: 0.0 + x == x for the products here, which are
     // never -0.0 -- quantities >= 0 times PositiveFloat weights, schema.py:174)
     double tw = (double)d[0] * skw[0];
@@ -1527,6 +1529,8 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
       u[sk] += rem[sk];
     }
     lost_cnt += remor != 0 ? 1 : 0;
+    }
+    }
   }
   PROF_ADD(q_all, PROF_NOW() - q_t0);
   PROF_FLUSH(10, q_all);
