@@ -1326,12 +1326,11 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
         wt = wl ? ex / group_np_sum<GW>(ex, W) : 0.0;
       }
       // (a closest-warehouse share is 1.0 and 1.0 * x == x: one update form serves every type)
-      if (wt != 0.0) {
-        pen += wt * upen;
-        if (dbg && info.lost_sales)
+      // (unconditional: a zero share adds a zero product, which leaves pen (>= +0.0) unchanged)
+      pen += wt * upen;
+      if (dbg && info.lost_sales && wt != 0.0)
 #pragma unroll
-          for (int sk = 0; sk < K; sk++) info.lost_sales[e * WK + w * K + sk] += wt * (double)u[sk];
-      }
+        for (int sk = 0; sk < K; sk++) info.lost_sales[e * WK + w * K + sk] += wt * (double)u[sk];
     }
     // home-region features: incoming demand and units shipped home (multi_env.py:767-773)
     if (r == myhome) {
@@ -1397,9 +1396,10 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
 #endif
     if (r != cur) {
       if (cur >= 0) finalize(cur);
-      if (r >= 0 && wl) {
-        cof = cost_of(r);
-        cov = cost_ov(r);
+      {  // (at clamped indices, no branch: the values for r = -1 or a lane past W are never used)
+        const int rr = r >= 0 ? r : 0, wc = wl ? w : 0;
+        cof = TAB ? lof[rr * W + wc] : gp(c.ofT)[rr * W + wc];
+        cov = TAB ? lov[rr * W + wc] : gp(c.ovT)[rr * W + wc];
       }
       cur = r;
       lost_cnt = 0;
