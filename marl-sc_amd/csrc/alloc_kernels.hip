@@ -172,6 +172,7 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
     const int v = __shfl_xor(wmax, o);
     wmax = v > wmax ? v : wmax;
   }
+  wmax = __builtin_amdgcn_readfirstlane(wmax);  // (uniform: a scalar loop bound, no lane masks per order)
 
   const int maxwh = c.max_wh, lost_type = c.lost_type, pps = c.pen_per_sku;
   const double alpha = sgpr_d(c.alpha);
@@ -324,19 +325,19 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
 #pragma unroll
       for (int sk = 0; sk < K; sk++) shc[sk] = 0;
     }
-    if (oi >= n_orders) continue;
+    // (structured ifs and one exit per loop, not continue / break: every exit is a latch whose lane
+    // masks the loops merge at each order and round; an empty order needs no test of its own -- no
+    // candidate, so its first round ends the loop, and with nothing unfulfilled it is never lost)
+    if (oi < n_orders) {
     int d[K], rem[K];
-    bool any_d = false;
     double tw = 0.0;  // order.sku_demands.dot(sku_weights) (demand_allocator.py:167)
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
       d[sk] = ur.h[1 + sk];
       rem[sk] = d[sk];
       dsum[sk] += d[sk];
-      any_d |= d[sk] > 0;
       tw += (double)d[sk] * skw[sk];
     }
-    if (!any_d) continue;  // an empty order ships nothing and is never lost
     // demand_allocator.py:168-172; every row is read first (unconditionally: the LDS table is
     // padded to MW, the global one clamped), so the loads overlap instead of each waiting alone
     double2 trow[MWL];
@@ -346,14 +347,17 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
 #pragma unroll
     for (int i = 0; i < MWL; i++) cost[i] = gw(i) < W ? trow[i].x + trow[i].y * tw : INFINITY;
     int used = 0;
-    for (;;) {
+    bool open = true;
+    while (open) {
       // candidates: warehouses holding a still-needed SKU (a warehouse that shipped already has
       // nothing left the order needs: fill = min(rem, inv) zeroes one of the two for every SKU;
       // a warehouse with nothing to give is skipped without counting towards max_splits)
       uint32_t cand = 0u;
 #pragma unroll
       for (int sk = 0; sk < K; sk++) cand |= rem[sk] > 0 ? stock[sk] : 0u;
-      if (LPE == 1 && cand == 0u) break;
+      if (LPE == 1 && cand == 0u) {
+        open = false;
+      } else {
       // cheapest candidate, lowest index on ties (the stable argsort order the fixtures assert)
       double best = INFINITY;
       int b = LPE == 1 ? 0 : SENT;
@@ -371,8 +375,10 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
         };
         mn(dpp_x<0>(best), dpp_x<0>(b));
         if constexpr (LPE == 4) mn(dpp_x<1>(best), dpp_x<1>(b));
-        if (b == SENT) break;  // nobody in the group holds a still-needed SKU
       }
+      if (LPE > 1 && b == SENT) {  // nobody in the group holds a still-needed SKU
+        open = false;
+      } else {
       const bool own = (b & (LPE - 1)) == jl;
       const int ib = b >> LSH;
       // every LDS value of warehouse b is read in one batch (one wait), then written back: shipped
@@ -439,18 +445,22 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
       }
       rtot += fs;
       used++;
+      open = !(done || used >= maxwh);
 #ifdef MSC_AL_ABL_ONEROUND  // (timing ablation only: results wrong)
-      break;
+      open = false;
 #endif
-      if (done || used >= maxwh) break;
+      }
+      }
     }
-    bool anyrem = false;
+    // (rem >= 0 throughout: every fill is min(rem, inv) with inv >= 0)
+    int remor = 0;
 #pragma unroll
     for (int sk = 0; sk < K; sk++) {
-      anyrem |= rem[sk] > 0;
-      u[sk] += rem[sk] > 0 ? rem[sk] : 0;
+      remor |= rem[sk];
+      u[sk] += rem[sk];
     }
-    lost_cnt += anyrem ? 1 : 0;
+    lost_cnt += remor != 0 ? 1 : 0;
+    }
   }
 
   if (!ev) return;
