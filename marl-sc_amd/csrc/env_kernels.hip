@@ -1477,8 +1477,19 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
         for (int j = 0; j < NP; j++) pk[j] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)pk[j]);
       }
 #else
+      // the NP words' OR butterflies interleaved stage by stage: each word's DPP reads a result two
+      // instructions old instead of the one just written, so no s_nop fills the DPP hazard
+      {
+        auto stage = [&](auto f) {
 #pragma unroll
-      for (int j = 0; j < NP; j++) pk[j] = (unsigned)group_reduce<GW>((int)pk[j], [](int a, int b) { return a | b; });
+          for (int j = 0; j < NP; j++) pk[j] |= (unsigned)f((int)pk[j]);
+        };
+        stage([](int v) { return dpp_x<0>(v); });
+        if constexpr (GW >= 4) stage([](int v) { return dpp_x<1>(v); });
+        if constexpr (GW >= 8) stage([](int v) { return dpp_x<2>(v); });
+        if constexpr (GW >= 16) stage([](int v) { return dpp_x<3>(v); });
+        if constexpr (GW >= 32) stage([](int v) { return dpp_x<4>(v); });
+      }
 #endif
       bool done = true;
 #pragma unroll
