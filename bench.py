@@ -213,8 +213,25 @@ def time_rollout(envs, module, T: int, world: int, seed: int, warm: int = 1, rep
     for x in el:
         x.check()
     if with_window:
-        return dt, {k: sum(w[k] for w in ww) for k in ww[0]}
+        return dt, merge_windows(ww, [x.n_envs for x in el])
     return dt
+
+
+def merge_windows(ww: list, n_envs: list) -> dict:
+    """One `window` object for env handles stepped together (rollout lanes): the integer counters
+    summed, `ahead_change_steps` recomputed over all their envs; the trace form when no handle had
+    generation work (empirical demand)."""
+    if all(w.get("ahead_change_steps") is None for w in ww):
+        out = dict(ww[0])
+        for k in ("env_steps_timed",):
+            out[k] = sum(int(w[k]) for w in ww)
+        return out
+    keys = ("ea_launches_in_window", "ea_env_steps_in_window", "demand_launches_in_window",
+            "demand_env_steps_in_window", "env_steps_timed")
+    out = {k: sum(int(w.get(k, 0)) for w in ww) for k in keys}
+    out["steps_in_window"] = max(int(w["steps_in_window"]) for w in ww)
+    out["ahead_change_steps"] = round((out["demand_env_steps_in_window"] - out["env_steps_timed"]) / max(1, sum(n_envs)), 1)
+    return out
 
 
 def c2_line(args, rank: int):
@@ -313,7 +330,7 @@ def c2_line(args, rank: int):
 def c5_line(args, rank: int):
     """BASELINE configs[4]: 16 agents x 256 regions x 5 SKUs, 8,192 envs, empirical demand traces (a
     synthetic preprocessor frame of ~200-1,000 orders per step), excluded-region mapping shape; the
-    env step only (its MAPPO rollout is `python bench.py --config c5`)."""
+    env step, then its MAPPO rollout (the line's `rollout` object)."""
     import torch
     from marlsc import make_synthetic_env_config
     from marlsc.seeding import default_train_seed
@@ -334,6 +351,17 @@ def c5_line(args, rank: int):
     env.reset()
     steps = max(100, args.steps)
     dt, tm = time_env(env, pool, steps, args.warmup, 1)
+    # configs[4] names a MAPPO rollout: the reference's config_files/algorithms/mappo.yaml (actor on the
+    # local obs, critic on local || global, mappo.yaml:31-32) over the same envs
+    t_roll, roll_win, rc = 0.0, None, None
+    if args.rollout_T > 0:
+        import yaml
+        from marlsc.rollout import ActorCritic, RolloutConfig
+        rc = RolloutConfig.from_algorithm_config(yaml.safe_load(open(REPO / "config_files/algorithms/mappo.yaml")))
+        torch.manual_seed(0)
+        module = ActorCritic(spec.local_obs_dim, spec.local_obs_dim * spec.W, spec.K, rc).cuda()
+        t_roll, roll_win = time_rollout(env, module, args.rollout_T, 1, seed=rank, warm=1, reps=2, with_window=True)
+        del module
     env.close()
     mean_orders = float(spec.trace["offsets"][-1]) / spec.trace["n_rows"]
     out = {"workload": f"InventoryEnvironment.step x {E} envs/GPU, {spec.W} agents x {spec.R} regions x {spec.K} SKUs, "
@@ -342,6 +370,18 @@ def c5_line(args, rank: int):
            "steps": steps, "warmup": args.warmup, "obs_normalization": meta.get("obs_normalization", "off"),
            "host_ms_per_step": round(tm["host_ms_per_step"], 4), "enqueue_ms_per_step": round(tm["enqueue_ms_per_step"], 4),
            "kernels_ms": {"step_kernels": round(tm["step_ms"], 4)}, "window": tm["window"]}
+    if rc is not None:
+        a_h, c_h = rc.actor["hidden_sizes"], rc.critic["hidden_sizes"]
+        out["rollout"] = {"value": round(E * spec.W * args.rollout_T / t_roll, 1), "unit": "agent-steps/s",
+                          "ms_per_step": round(t_roll / args.rollout_T * 1e3, 4), "T": args.rollout_T, "reps": 2,
+                          "policy": f"MAPPO (config_files/algorithms/mappo.yaml): actor {spec.local_obs_dim}-"
+                                    f"{'-'.join(map(str, a_h))}-{spec.K}, critic {spec.local_obs_dim * (1 + spec.W)}-"
+                                    f"{'-'.join(map(str, c_h))}-1 on local || global, fp32, parameter sharing, "
+                                    f"obs {meta.get('obs_normalization', 'off')}",
+                          "includes": "env step, actor forward + Gaussian sampling, MAPPO critic (first layer split: "
+                                      "global block once per env), buffer writes, truncation bootstrap, GAE kernel, "
+                                      "adv-norm statistics + normalise",
+                          "window": roll_win}
     # the step kernels (no demand kernel: the trace window is read inside step_a) against the VALU
     # issue peak and their HBM bytes, from the PMC passes of this workload (profiles/traffic.json)
     tj = Path(args.traffic_json)
@@ -365,6 +405,13 @@ def c5_line(args, rank: int):
     return out
 
 
+def ea_fraction_per_rank() -> float:
+    """The episode-ahead memory budget of a rank's handle (marlsc.dist.ea_mem_fraction): ranks sharing
+    one card split the library's default quarter of its free memory."""
+    from marlsc.dist import ea_mem_fraction
+    return ea_mem_fraction()
+
+
 def strong_line(args, rank: int, world: int, spec, meta: dict) -> dict:
     """BASELINE configs[3] as stated: `--strong-envs` envs in total (32,768) sharded over the N ranks,
     rank g owning global env ids [g * E / N, (g + 1) * E / N) (every env seeded from
@@ -377,12 +424,13 @@ def strong_line(args, rank: int, world: int, spec, meta: dict) -> dict:
     import torch.distributed as dist
     from marlsc.seeding import default_train_seed
     from marlsc.vec_env import VecInventoryEnv
+    from marlsc.dist import shard
     E_tot = args.strong_envs
     if E_tot % world:
         raise SystemExit(f"--strong-envs {E_tot} is not divisible by {world} ranks")
-    n = E_tot // world
+    n, off = shard(E_tot, "strong", rank, world)
     env = VecInventoryEnv(None, n, spec=spec, device=torch.cuda.current_device(), base_seed=default_train_seed(42),
-                          env_index_offset=rank * n)
+                          env_index_offset=off, ea_mem_fraction=ea_fraction_per_rank())
     g = torch.Generator(device="cuda").manual_seed(4321 + rank)
     pool = [torch.rand((n, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
     env.reset()
@@ -541,7 +589,9 @@ def main():
     # episode-ahead buffers (the memory budget picks the slots: 4 at 32,768 envs) for the steady-state
     # line below; the headline steps with per-step pipelined demand (EA paused)
     want_ea = world == 1 and args.config == "c3" and args.ea_line
-    env = VecInventoryEnv(None, E, spec=spec, device=dev, base_seed=default_train_seed(42), env_index_offset=rank * E,
+    from marlsc.dist import shard
+    env = VecInventoryEnv(None, E, spec=spec, device=dev, base_seed=default_train_seed(42),
+                          env_index_offset=shard(E, "weak", rank, world)[1], ea_mem_fraction=ea_fraction_per_rank(),
                           episode_ahead=16 if want_ea else None)
     if env.ea_slots and E > 8192:
         env.set_episode_ahead(False)

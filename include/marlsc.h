@@ -175,6 +175,13 @@ int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t
                  int32_t* n_regions, int32_t* local_obs_dim, int32_t* n_features,
                  int32_t* max_expected_lead_time, int32_t* ea_slots);
 
+/* Diagnostic (no reference counterpart: the reference has one code path): the kernels this handle
+ * runs, chosen at create time from its shape and the MSC_* knobs. Writes up to n of
+ * {alloc (0 lane, 1 group, 2 scan), envs sorted by order count, phase A fused, phase C fused,
+ *  group kernel cost tables in LDS, lane-group width, episode-ahead slots, demand (0 unit parser,
+ *  5 park4, 7 split parser), equal sampler parameters (UNI)}; returns the count written. */
+int msc_env_kernel_choice(const msc_env* env, int32_t* out, int32_t n);
+
 #define MSC_RESET_EVAL_RESTART 1  /* reset(seed=...) of a construction-seeded eval env: counter -> 0 */
 
 /* Reset envs with mask[i] != 0 (mask == NULL: all). new_root_seeds == NULL follows the

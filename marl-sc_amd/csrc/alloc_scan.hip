@@ -466,8 +466,10 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
   int inv[NS], inv0[NS], qsr[NS], u[NS], dsum[NS], inc_h[NS], shh_h[NS], fi[NS];
   double lost[NS], ovacc[NS];
   const int t_now = FC ? __builtin_amdgcn_readfirstlane(s.t[e]) : 0;
-  // FA: phase A (step_a_kernel's per-(SKU, warehouse) work) on this lane's slot; the ring after it
-  // stays in registers for phase C; the warehouse's inbound cost reaches lane w (sg == 0)
+  // FA: phase A (step_a_kernel's per-(SKU, warehouse) work) on this lane's slot; the warehouse's
+  // inbound cost reaches lane w (sg == 0). The updated ring goes back to global memory and phase C
+  // reloads it after the allocation (the RING registers are not kept live across the order loop, whose
+  // VGPR budget sets the waves per SIMD; the reload hits L2)
   double inb_a = 0.0;
   if constexpr (FA) {
     const int RING = c.RING, slot = t_now % RING;

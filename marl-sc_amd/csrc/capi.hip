@@ -501,7 +501,7 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
       int ncu = 256;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
       int gw = W <= 2 ? 2 : W <= 4 ? 4 : W <= 8 ? 8 : W <= 16 ? 16 : 32;
-      if (const char* g = getenv("MSC_SB_GW")) gw = atoi(g) > gw && atoi(g) <= 32 ? atoi(g) : gw;
+      if (c.sb_gw > gw) gw = c.sb_gw;  // (the validated MSC_SB_GW: the group width launch_step_k uses)
       // (blocks of 8 waves for 16- and 32-lane groups with the tables, else 4: step_b_waves)
       const int bw = gw >= 16 ? 8 : 4;
       const int64_t blocks = (n_envs * gw + 64 * bw - 1) / (64 * bw), per_cu = (blocks + ncu - 1) / ncu;
@@ -880,6 +880,19 @@ int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t
   if (max_lead) *max_lead = env->c.Lmax;
   if (ea_slots) *ea_slots = env->ea_enabled ? env->c.ea_S : 0;
   return 0;
+}
+
+int msc_env_kernel_choice(const msc_env* env, int32_t* out, int32_t n) {
+  if (!env || (!out && n > 0)) return set_err(-1, "null argument");
+  const EnvConst& c = env->c;
+  const int W = c.W;
+  int gw = W <= 2 ? 2 : W <= 4 ? 4 : W <= 8 ? 8 : W <= 16 ? 16 : 32;
+  if (c.sb_gw > gw) gw = c.sb_gw;
+  const int32_t v[9] = {c.alloc_impl, c.alloc_sort, c.fuse_a, c.fuse_c, c.sb_tab, c.alloc_impl == 1 ? gw : 0,
+                        env->ea_enabled ? c.ea_S : 0, c.demand_impl, c.demand_uni};
+  const int m = n < 9 ? n : 9;
+  for (int i = 0; i < m; i++) out[i] = v[i];
+  return m;
 }
 
 int msc_env_reset(msc_env* env, const uint8_t* mask, const uint32_t* new_root_seeds, int32_t flags, float* obs,

@@ -185,6 +185,16 @@ class VecInventoryEnv:
         abi.check(abi.lib().msc_env_ea_memory(self._h, C.byref(b), C.byref(a)))
         return {"budget": b.value, "allocated": a.value, "slots": self.ea_slots}
 
+    def kernel_choice(self) -> Dict[str, int]:
+        """The kernels this handle runs (msc_env_kernel_choice), chosen at create time by shape."""
+        keys = ("alloc", "alloc_sort", "fuse_a", "fuse_c", "group_tables_lds", "group_width", "ea_slots",
+                "demand_impl", "demand_uni")
+        buf = (C.c_int32 * len(keys))()
+        n = abi.lib().msc_env_kernel_choice(self._h, buf, len(keys))
+        if n < 0:
+            abi.check(n)
+        return {k: int(buf[i]) for i, k in enumerate(keys[:n])}
+
     def read_timing_ea(self) -> Dict[str, float]:
         """Episode-ahead demand (msc_env_read_timing_ea): mean device ms of the timed episode
         generation launches, their count, slots per env (0: off) and whether the current episode

@@ -59,7 +59,7 @@ def _set_alloc(monkeypatch, param):
         monkeypatch.setenv("MSC_EA", ea)
 
 
-@pytest.fixture(params=["lane", "group", "group_sorted", "scan", "scan_ea0", "scan_nofc", "scan_nofa"])
+@pytest.fixture(params=["lane", "group", "group_sorted", "group_nofc", "scan", "scan_ea0", "scan_nofc", "scan_nofa"])
 def alloc_impl(request, monkeypatch):
     # every phase-B allocation kernel (one env per lane / per lane group / per wave) against the same
     # references, with and without episode-ahead demand; msc_env_create picks by shape otherwise
@@ -171,6 +171,33 @@ def test_c5_shape_vs_oracle():
     cfg = make_synthetic_env_config(16, 256, 5, episode_length=12)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     _lockstep(spec, 64, 15, check_every=5)
+
+
+def test_c5_bench_geometry_vs_oracle_8192(monkeypatch):
+    # BASELINE configs[4] at its stated size, 8,192 envs x 16 x 256 x 5 with an empirical
+    # trace of ~200-1,000 orders per step and meanstd observations, through the library's own choice
+    # of kernels (what bench.py's c5 line runs: the group allocator over envs sorted by order count,
+    # 16-lane groups, 8-wave blocks with the cost tables in LDS, the interleaved wave mapping over 256
+    # blocks, phase C inside step_b), in lockstep with the oracle; 4-step episodes put an episode
+    # boundary inside steps 4 and 8 (the in-kernel reset and the trace window redraw)
+    from marlsc.synthetic import make_synthetic_trace
+    for k in ("MSC_ALLOC_IMPL", "MSC_ALLOC_LPE", "MSC_ALLOC_SORT", "MSC_OBS_STAGE", "MSC_OBS_RING_REG", "MSC_FUSE_C",
+              "MSC_FUSE_A", "MSC_EA", "MSC_SB_GW", "MSC_SB_TAB"):
+        monkeypatch.delenv(k, raising=False)
+    cfg = make_synthetic_env_config(16, 256, 5, episode_length=4)
+    cfg["components"]["demand_sampler"] = {"type": "empirical", "params": None}
+    meta = {"include_warehouse_id": True, "demand_trace": make_synthetic_trace(256, 5, 300, orders_per_step=(200, 1000), seed=0)}
+    nf = EnvSpec.from_config(cfg, meta).n_features
+    g = np.random.default_rng(21)
+    meta.update(obs_normalization="meanstd_custom",
+                obs_stats=(g.uniform(-2, 30, nf).astype(np.float32), g.uniform(0.5, 12, nf).astype(np.float32)))
+    spec = EnvSpec.from_config(cfg, meta)
+    probe = _vec(spec, 8192, base_seed=777)
+    kc = probe.kernel_choice()
+    probe.close()
+    assert kc["alloc"] == 1 and kc["alloc_sort"] == 1 and kc["fuse_c"] == 1, kc
+    assert kc["group_width"] == 16 and kc["group_tables_lds"] == 1, kc
+    _lockstep(spec, 8192, 11, seed=8, check_every=2)
 
 
 @pytest.mark.parametrize("name", ["c8_split", "variant_a", "variant_b", "variant_c", "repo_3wh5sku"])

@@ -426,3 +426,29 @@ def test_bench_window_accounting():
     assert drained["ahead_change_steps"] == -30.0
     trace = bench.window_work(z, dict(z, steps=7), 64, 7)
     assert trace["ahead_change_steps"] is None and trace["env_steps_timed"] == 448
+    # rollout lanes: the windows of several handles merged (the trace form, whose
+    # 'demand' is a string, and per-env averages that must not be added up)
+    merged_trace = bench.merge_windows([trace, trace], [64, 64])
+    assert merged_trace["ahead_change_steps"] is None and merged_trace["env_steps_timed"] == 896
+    a = bench.window_work(z, dict(z, ea_launches=2, ea_env_steps=64 * 100, steps=50), 64, 50)  # +50 per env
+    b = bench.window_work(z, dict(z, ea_launches=1, ea_env_steps=32 * 20, steps=50), 32, 50)   # -30 per env
+    m = bench.merge_windows([a, b], [64, 32])
+    assert m["ea_launches_in_window"] == 3 and m["env_steps_timed"] == 96 * 50
+    assert m["ahead_change_steps"] == round((64 * 100 + 32 * 20 - 96 * 50) / 96, 1)
+
+
+def test_dist_shard_partitions(monkeypatch):
+    """marlsc.dist.shard: weak and strong env-id partitions (bench.py, BASELINE configs[2] / [3]); the
+    episode-ahead budget split between ranks that share one card."""
+    from marlsc import dist
+    assert [dist.shard(32768, "strong", g, 4) for g in range(4)] == [(8192, g * 8192) for g in range(4)]
+    assert [dist.shard(32768, "weak", g, 4) for g in range(4)] == [(32768, g * 32768) for g in range(4)]
+    with pytest.raises(ValueError):
+        dist.shard(32768, "strong", 0, 3)
+    ids = np.concatenate([np.arange(o, o + n) for n, o in (dist.shard(32768, "strong", g, 8) for g in range(8))])
+    assert np.array_equal(ids, np.arange(32768))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    monkeypatch.setattr(dist.torch.cuda, "device_count", lambda: 1)
+    assert dist.ranks_per_device() == 4 and dist.ea_mem_fraction() == 0.0625
+    monkeypatch.setattr(dist.torch.cuda, "device_count", lambda: 8)
+    assert dist.ranks_per_device() == 1 and dist.ea_mem_fraction() == 0.25
