@@ -388,6 +388,20 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     c.uni_thr_o = enlam_o[0];
     c.uni_thr_m = p_skip[0];
     c.uni_thr_q = enlam_q[0];
+    // demand_v2_kernel (demand_v2.hip): its f32 chain decides "prod > exp(-lambda)" only outside a
+    // band of relative width 2^-16 around the threshold (both bounds rounded outward to f32); the SKU
+    // draw U = k 2^-53 < p <=> k < ceil(p 2^53), exact on the integer
+    auto f_up = [](double v) { float f = (float)v; return (double)f < v ? nextafterf(f, INFINITY) : f; };
+    auto f_dn = [](double v) { float f = (float)v; return (double)f > v ? nextafterf(f, -INFINITY) : f; };
+    // (MSC_V2_BAND=b widens the band to 2^-b, b in [2, 16]: tests drive the exact recomputation with it)
+    int band = 16;
+    if (const char* vb = getenv("MSC_V2_BAND")) band = atoi(vb) >= 2 && atoi(vb) <= 16 ? atoi(vb) : band;
+    const double bw = ldexp(1.0, -band);
+    c.v2_thr[0] = f_up(enlam_o[0] * (1.0 + bw));
+    c.v2_thr[1] = f_dn(enlam_o[0] * (1.0 - bw));
+    c.v2_thr[2] = f_up(enlam_q[0] * (1.0 + bw));
+    c.v2_thr[3] = f_dn(enlam_q[0] * (1.0 - bw));
+    c.v2_k53 = (uint64_t)ceil(ldexp(p_sku[0] < 2.0 ? p_sku[0] : 2.0, 53));
   } else if (d->demand_type == MSC_DEMAND_EMPIRICAL) {
     const int rows = d->trace_n_rows;
     if (rows < d->episode_length) return set_err(-1, "trace has %d timesteps < episode_length %d", rows, d->episode_length);
@@ -415,7 +429,12 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     const char* impl = getenv("MSC_DEMAND_IMPL");
     // default (0): the unit-per-round parser; "ab" the split chain / bookkeeper parser
     // (demand_ab_kernel: measured slower), "park4" the round-1 parser
-    c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : impl && strcmp(impl, "ab") == 0 ? 7 : 0;
+    c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : impl && strcmp(impl, "ab") == 0 ? 7
+                  : impl && strcmp(impl, "v2") == 0 ? 8 : 0;
+    // demand_v2_kernel's generator refill per chunk (positions per lane; the parser consumes ~18 at
+    // 8 x 64 x 5): MSC_V2_QUOTA
+    c.v2_quota = 20;
+    if (const char* vq = getenv("MSC_V2_QUOTA")) c.v2_quota = atoi(vq) >= 8 && atoi(vq) <= 64 ? atoi(vq) : c.v2_quota;
     const char* gen = getenv("MSC_DEMAND_GEN");
     // (5 and 7: A/B instantiations for 5 SKUs only, more generator waves per 64 envs)
     c.demand_gen = gen && ((atoi(gen) >= 1 && atoi(gen) <= 3) || (K == 5 && (atoi(gen) == 5 || atoi(gen) == 7))) ? atoi(gen) : 3;

@@ -57,6 +57,12 @@ struct EnvConst {
   int64_t ea_cap;       // episode-ahead demand: order records per (slot, env) episode
   double scale, alpha, hold_scalar, pen_scalar;
   double uni_thr_o, uni_thr_m, uni_thr_q;  // demand_uni: exp(-lambda_orders), p_skip, exp(-lambda_quantity)
+  // demand_v2_kernel (demand_v2.hip, f32 ring): the f32 chain's decision thresholds around exp(-lambda)
+  // {orders hi, orders lo, quantity hi, quantity lo}, the exact SKU-draw bound ceil(p * 2^53) on the
+  // 53-bit draw, and the generators' refill quota per chunk
+  float v2_thr[4];
+  uint64_t v2_k53;
+  int32_t v2_quota;
   const MSC_G double* act_param;   // [K]
   const MSC_G int32_t* init_vals;  // [W*K]
   const MSC_G double* hold;        // [K]
@@ -215,6 +221,9 @@ hipError_t launch_demand_seq(const EnvConst& c, const DevEnv* d, hipStream_t st,
 hipError_t launch_poisson_draws(uint64_t* state, const PtrsConst* ptrs, const double* enlam, int64_t n_lam, int64_t n,
                                 int64_t* out, hipStream_t st);
 hipError_t launch_demand_ab(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea);
+// demand_v2.hip: the f32-ring Poisson demand kernel (equal sampler parameters, <= 8 SKUs)
+bool demand_v2_supported(const EnvConst& c);
+hipError_t launch_demand_v2(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea);
 int order_record_vec4(int K);
 // gae.hip
 hipError_t launch_gae(const float* r, const float* v, const float* nv, const uint8_t* term, const uint8_t* trunc,

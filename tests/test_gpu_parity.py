@@ -728,6 +728,47 @@ def test_split_parser_demand_vs_oracle(monkeypatch, ea):
     _lockstep(spec, 192, 21, seed=6, check_every=4)
 
 
+@pytest.mark.parametrize("ea", ["0", "1"])
+@pytest.mark.parametrize("band,quota", [(None, None), ("3", None), (None, "8"), (None, "40")])
+def test_demand_v2_vs_oracle(monkeypatch, ea, band, quota):
+    # the f32-ring demand kernel (csrc/demand_v2.hip): f32 draws with the SKU draw in the sign bit, a
+    # 128-position ring, the f32 Poisson chain decided outside a band around exp(-lambda) and the exact
+    # recomputation (jump-ahead + numpy's f64 chain) inside it; per step and episode-ahead, in lockstep
+    # with the oracle across episode boundaries. band 2^-3 sends a large share of the Poisson rounds
+    # through the exact path; quota 8 / 40 exercise the generators' top-up barrier and a full ring
+    monkeypatch.setenv("MSC_DEMAND_IMPL", "v2")
+    monkeypatch.setenv("MSC_EA", ea)
+    if band:
+        monkeypatch.setenv("MSC_V2_BAND", band)
+    if quota:
+        monkeypatch.setenv("MSC_V2_QUOTA", quota)
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=9)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    env, _ = _lockstep(spec, 192, 21, seed=7, check_every=4)
+    assert env.kernel_choice()["demand_impl"] == 8
+
+
+@pytest.mark.parametrize("K,lo,lq,p", [(1, 4.0, 5.0, 0.667), (3, 2.5, 9.5, 0.3), (8, 1.5, 9.9, 1.0), (6, 9.9, 0.4, 0.9)])
+def test_demand_v2_shapes_and_rates_vs_oracle(monkeypatch, K, lo, lq, p):
+    # the f32-ring kernel at other SKU counts and rates: lambda 9.5-9.9 (units past 24 draws, decided
+    # exactly), p = 1 (every SKU drawn: the integer bound ceil(p 2^53) = 2^53), tiny quantity rates
+    monkeypatch.setenv("MSC_DEMAND_IMPL", "v2")
+    cfg = make_synthetic_env_config(5, 24, K, episode_length=7, lambda_orders=lo, lambda_quantity=lq,
+                                    probability_skus=p)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    env, _ = _lockstep(spec, 130, 16, seed=K, check_every=3)
+    assert env.kernel_choice()["demand_impl"] == 8
+
+
+@pytest.mark.usefixtures("alloc_impl")
+def test_demand_v2_bench_shape_vs_oracle(monkeypatch):
+    # BASELINE configs[2] shape with every allocation kernel, 512 envs, 110 steps (one auto-reset)
+    monkeypatch.setenv("MSC_DEMAND_IMPL", "v2")
+    cfg = make_synthetic_env_config(8, 64, 5)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 512, 110, seed=11, check_every=10)
+
+
 def test_episode_ahead_runtime_switch_stays_exact(monkeypatch):
     # msc_env_set_episode_ahead: episode-ahead demand switched off mid-episode (per-step pipelined
     # demand from that step on) and back on (restarting at the next common episode start) leaves
