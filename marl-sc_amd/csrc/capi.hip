@@ -429,8 +429,11 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     const char* impl = getenv("MSC_DEMAND_IMPL");
     // default (0): the unit-per-round parser; "ab" the split chain / bookkeeper parser
     // (demand_ab_kernel: measured slower), "park4" the round-1 parser
-    c.demand_impl = impl && strcmp(impl, "park4") == 0 ? 5 : impl && strcmp(impl, "ab") == 0 ? 7
-                  : impl && strcmp(impl, "v2") == 0 ? 8 : 0;
+    // default (9): the short-round unit parser (demand_v3.hip) where the sampler's parameters are equal
+    // in every region and SKU, the unit parser otherwise (0, "unit" forces it; C3 demand 0.787 -> 0.758
+    // ms, C2 205 -> 208.7 M, profiles/r06/ab_demand_v3.txt)
+    c.demand_impl = !impl ? 9 : strcmp(impl, "park4") == 0 ? 5 : strcmp(impl, "ab") == 0 ? 7
+                  : strcmp(impl, "v2") == 0 ? 8 : strcmp(impl, "v3") == 0 ? 9 : 0;
     // demand_v2_kernel's generator refill per chunk (positions per lane; the parser consumes ~18 at
     // 8 x 64 x 5): MSC_V2_QUOTA
     c.v2_quota = 20;

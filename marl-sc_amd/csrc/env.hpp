@@ -224,6 +224,11 @@ hipError_t launch_demand_ab(const EnvConst& c, const DevEnv* d, hipStream_t st, 
 // demand_v2.hip: the f32-ring Poisson demand kernel (equal sampler parameters, <= 8 SKUs)
 bool demand_v2_supported(const EnvConst& c);
 hipError_t launch_demand_v2(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea);
+// demand_v3.hip: the unit parser with a shorter round (equal sampler parameters, <= 8 SKUs), and the
+// dispatcher of the alternative demand kernels (c.demand_impl 8 / 9)
+bool demand_v3_supported(const EnvConst& c);
+hipError_t launch_demand_v3(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea);
+hipError_t launch_demand_alt(const EnvConst& c, const DevEnv* d, hipStream_t st, const EaLaunch* ea);
 int order_record_vec4(int K);
 // gae.hip
 hipError_t launch_gae(const float* r, const float* v, const float* nv, const uint8_t* term, const uint8_t* trunc,

@@ -1805,8 +1805,9 @@ static hipError_t launch_split_demand(const EnvConst& c, const DevEnv* d, hipStr
   if (G == 3 && c.demand_impl == 7 && demand_ab_supported(c)) {  // the split parser (demand_ab.hip, A/B)
     return launch_demand_ab(c, d, st, ea);
   }
-  if (G == 3 && c.demand_impl == 8 && demand_v2_supported(c)) {  // the f32-ring parser (demand_v2.hip)
-    return launch_demand_v2(c, d, st, ea);
+  if (G == 3 && c.demand_impl >= 8) {  // the f32-ring / short-round parsers (demand_v2.hip, demand_v3.hip)
+    const hipError_t ealt = launch_demand_alt(c, d, st, ea);
+    if (ealt != hipErrorNotSupported) return ealt;
   }
   const size_t tab = (size_t)(2 + K) * c.R * sizeof(double);
   const bool t = park_lds_tables(c);

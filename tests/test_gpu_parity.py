@@ -728,6 +728,22 @@ def test_split_parser_demand_vs_oracle(monkeypatch, ea):
     _lockstep(spec, 192, 21, seed=6, check_every=4)
 
 
+@pytest.mark.parametrize("impl", ["v3", "unit"])
+@pytest.mark.parametrize("ea", ["0", "1"])
+def test_demand_v3_vs_oracle(monkeypatch, ea, impl):
+    # the short-round unit parser (csrc/demand_v3.hip, the default for equal sampler parameters) and
+    # the unit parser it replaced (MSC_DEMAND_IMPL=unit: its constant-threshold form stays under test),
+    # per step and episode-ahead (4-step chunks continue from the recorded stream position and record
+    # count), in lockstep with the oracle
+    monkeypatch.setenv("MSC_DEMAND_IMPL", impl)
+    monkeypatch.setenv("MSC_EA", ea)
+    monkeypatch.setenv("MSC_EA_CHUNK", "4")
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=9)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    env, _ = _lockstep(spec, 192, 21, seed=9, check_every=4)
+    assert env.kernel_choice()["demand_impl"] == (9 if impl == "v3" else 0)
+
+
 @pytest.mark.parametrize("ea", ["0", "1"])
 @pytest.mark.parametrize("band,quota", [(None, None), ("3", None), (None, "8"), (None, "40")])
 def test_demand_v2_vs_oracle(monkeypatch, ea, band, quota):
@@ -748,22 +764,25 @@ def test_demand_v2_vs_oracle(monkeypatch, ea, band, quota):
     assert env.kernel_choice()["demand_impl"] == 8
 
 
+@pytest.mark.parametrize("impl", ["v2", "v3"])
 @pytest.mark.parametrize("K,lo,lq,p", [(1, 4.0, 5.0, 0.667), (3, 2.5, 9.5, 0.3), (8, 1.5, 9.9, 1.0), (6, 9.9, 0.4, 0.9)])
-def test_demand_v2_shapes_and_rates_vs_oracle(monkeypatch, K, lo, lq, p):
-    # the f32-ring kernel at other SKU counts and rates: lambda 9.5-9.9 (units past 24 draws, decided
-    # exactly), p = 1 (every SKU drawn: the integer bound ceil(p 2^53) = 2^53), tiny quantity rates
-    monkeypatch.setenv("MSC_DEMAND_IMPL", "v2")
+def test_demand_v2_shapes_and_rates_vs_oracle(monkeypatch, impl, K, lo, lq, p):
+    # the f32-ring kernel (v2) at other SKU counts and rates: lambda 9.5-9.9 (units past 24 draws,
+    # decided exactly), p = 1 (every SKU drawn: the integer bound ceil(p 2^53) = 2^53), tiny quantity
+    # rates; the same shapes through the short-round unit parser (v3, csrc/demand_v3.hip)
+    monkeypatch.setenv("MSC_DEMAND_IMPL", impl)
     cfg = make_synthetic_env_config(5, 24, K, episode_length=7, lambda_orders=lo, lambda_quantity=lq,
                                     probability_skus=p)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     env, _ = _lockstep(spec, 130, 16, seed=K, check_every=3)
-    assert env.kernel_choice()["demand_impl"] == 8
+    assert env.kernel_choice()["demand_impl"] == (8 if impl == "v2" else 9)
 
 
+@pytest.mark.parametrize("impl", ["v2", "v3"])
 @pytest.mark.usefixtures("alloc_impl")
-def test_demand_v2_bench_shape_vs_oracle(monkeypatch):
+def test_demand_v2_bench_shape_vs_oracle(monkeypatch, impl):
     # BASELINE configs[2] shape with every allocation kernel, 512 envs, 110 steps (one auto-reset)
-    monkeypatch.setenv("MSC_DEMAND_IMPL", "v2")
+    monkeypatch.setenv("MSC_DEMAND_IMPL", impl)
     cfg = make_synthetic_env_config(8, 64, 5)
     spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
     _lockstep(spec, 512, 110, seed=11, check_every=10)
