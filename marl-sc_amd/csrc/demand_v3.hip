@@ -9,8 +9,11 @@
 // bookkeeping the round executes:
 //  * the unit kind as three 0/1 flags (quantity, mask, order count) instead of a state enum compared
 //    in every settle;
-//  * the chain threshold chosen between exp(-lambda_o) and exp(-lambda_q) only (two selects): the
-//    SKU draws compare against p_skip in scalar registers;
+//  * the chain threshold chosen between exp(-lambda_o) and exp(-lambda_q) only (two selects, both
+//    held in VGPRs); the SKU draws compare against p_skip in scalar registers (carrying the SKU draw
+//    in the sign bit of the ring entry shortens the round by 15 instructions but costs the generators
+//    a compare and its hazard wait per draw: the kernel got slower, 0.758 -> 0.784 ms,
+//    profiles/r06/ab_demand_v3.txt -- the generators, not only the parser, set its pace);
 //  * record addresses from a clamped record index by one 64-bit multiply-add at each store, so
 //    neither store tests the capacity (an overflowing env rewrites its last record and raises the
 //    error flag, as before);
@@ -156,7 +159,11 @@ __global__ __launch_bounds__(BS * (1 + G)) __attribute__((amdgpu_waves_per_eu(MS
   }
   // (scalar loads of the descriptor, consumed before the loop: a vector load here would leave its
   // wait, vmcnt(0), inside the loop, where it also waits for every record store in flight)
-  const double thr_o = sgpr_d(c.uni_thr_o), thr_m = sgpr_d(c.uni_thr_m), thr_q = sgpr_d(c.uni_thr_q);
+  // (the two chain thresholds held in VGPRs: the per-round select would otherwise copy them from
+  // scalar registers every settle)
+  double thr_o = sgpr_d(c.uni_thr_o), thr_q = sgpr_d(c.uni_thr_q);
+  asm volatile("" : "+v"(thr_o), "+v"(thr_q));
+  const double thr_m = sgpr_d(c.uni_thr_m);
   const int R_s = __builtin_amdgcn_readfirstlane(c.R), cap_s = __builtin_amdgcn_readfirstlane(cap);
   const uint32_t rs32 = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rstride);  // (< 2^32: E * 16 * NV)
   // the current record: index min(n, cap) - 1 (clamped: an overflow rewrites the last record)

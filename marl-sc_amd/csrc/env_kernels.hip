@@ -1573,8 +1573,15 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
 // WB: the most waves a block has; blocks of <= 8 waves get up to 256 VGPRs per lane, so the
 // observation builder holds the pending ring in registers without spilling. One warehouse per wave
 // up to STEP_WAVES warehouses (LOOP: each wave takes w, w + WB, ...; see each_warehouse)
+#ifndef MSC_SC_WPE
+// waves per SIMD the 16-wave step_c form is compiled for: 5 (<= 96 VGPRs, some spilled) lets two of
+// its 8-wave blocks sit beside the pipelined demand kernel's waves on a CU; at 128 VGPRs only one did,
+// and step_c ran in two rounds of blocks (C3 pipelined step: 300 -> 230 us, profiles/r06/ab_step_c_wpe.txt)
+#define MSC_SC_WPE 5
+#endif
 template <int K, bool DBG, int WB = STEP_WAVES, bool LOOP = false>
-__global__ __launch_bounds__(BS * WB) void step_c_kernel(const DevEnv* __restrict__ dp, StepIO io) {
+__global__ __launch_bounds__(BS * WB) __attribute__((amdgpu_waves_per_eu(WB == STEP_WAVES && !LOOP ? MSC_SC_WPE : 1)))
+void step_c_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   constexpr int RREG = (WB <= 8 && K <= 8) ? OBS_RING_REG : 0;
   constexpr bool HSTAT = true;
   const EnvConst& c = dp->c;
