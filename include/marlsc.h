@@ -182,6 +182,13 @@ int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t
  *  5 park4, 7 split parser), equal sampler parameters (UNI)}; returns the count written. */
 int msc_env_kernel_choice(const msc_env* env, int32_t* out, int32_t n);
 
+/* Kernel-form options of a handle that change no result (diagnostic / tuning; no reference
+ * counterpart). MSC_OPT_STEP_C_FORM: the waves per SIMD the observation kernel is compiled for, 5
+ * (default: beside the pipelined demand kernel) or 4 (no register spills; the rollout collector's
+ * choice, with policy kernels between steps). Returns 0, or < 0 for an unknown key / value. */
+#define MSC_OPT_STEP_C_FORM 1
+int msc_env_set_option(msc_env* env, int32_t key, int32_t value);
+
 #define MSC_RESET_EVAL_RESTART 1  /* reset(seed=...) of a construction-seeded eval env: counter -> 0 */
 
 /* Reset envs with mask[i] != 0 (mask == NULL: all). new_root_seeds == NULL follows the

@@ -506,6 +506,8 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     // sampler draws its window start in phase A). MSC_FUSE_A=0 keeps the step_a kernel.
     c.fuse_a = c.alloc_impl == 2 && c.fuse_c && d->lead_type != MSC_LEAD_STOCHASTIC && d->demand_type == MSC_DEMAND_POISSON ? 1 : 0;
     c.sc_tab = 1;
+    c.sc_form = 5;
+    if (const char* sf = getenv("MSC_STEP_C_FORM")) c.sc_form = atoi(sf) == 4 ? 4 : 5;
     if (const char* st = getenv("MSC_SC_TAB")) c.sc_tab = atoi(st) != 0 ? 1 : 0;
     c.sb_gw = 0;
     if (const char* g = getenv("MSC_SB_GW")) {
@@ -1083,6 +1085,16 @@ int msc_env_set_chain_priority(msc_env* env, int32_t enabled) {
   for (int b = 0; b < 2; b++)
     HIP_TRY(hipMemcpy(&env->dev[b].c.chain_prio, &v, sizeof v, hipMemcpyHostToDevice));
   return 0;
+}
+
+int msc_env_set_option(msc_env* env, int32_t key, int32_t value) {
+  if (!env) return set_err(-1, "null env");
+  if (key == MSC_OPT_STEP_C_FORM) {
+    if (value != 4 && value != 5) return set_err(-1, "MSC_OPT_STEP_C_FORM must be 4 or 5");
+    env->c.sc_form = value;  // (host-side launch choice: the device descriptor does not carry it)
+    return 0;
+  }
+  return set_err(-1, "unknown option %d", key);
 }
 
 int msc_env_set_timing(msc_env* env, int32_t max_steps) {

@@ -1576,11 +1576,14 @@ __global__ __launch_bounds__(64 * step_b_waves(GW, TAB)) __attribute__((amdgpu_w
 #ifndef MSC_SC_WPE
 // waves per SIMD the 16-wave step_c form is compiled for: 5 (<= 96 VGPRs, some spilled) lets two of
 // its 8-wave blocks sit beside the pipelined demand kernel's waves on a CU; at 128 VGPRs only one did,
-// and step_c ran in two rounds of blocks (C3 pipelined step: 300 -> 230 us, profiles/r06/ab_step_c_wpe.txt)
+// and step_c ran in two rounds of blocks (C3 pipelined step: 300 -> 230 us, profiles/r06/ab_step_c_wpe.txt).
+// In the rollout (policy kernels between steps) the 128-VGPR form without spills is faster (1.18 ->
+// 1.14 ms per MAPPO step): c.sc_form picks it (msc_env_set_option MSC_OPT_STEP_C_FORM, set by the
+// rollout collector)
 #define MSC_SC_WPE 5
 #endif
-template <int K, bool DBG, int WB = STEP_WAVES, bool LOOP = false>
-__global__ __launch_bounds__(BS * WB) __attribute__((amdgpu_waves_per_eu(WB == STEP_WAVES && !LOOP ? MSC_SC_WPE : 1)))
+template <int K, bool DBG, int WB = STEP_WAVES, bool LOOP = false, int SCW = MSC_SC_WPE>
+__global__ __launch_bounds__(BS * WB) __attribute__((amdgpu_waves_per_eu(WB == STEP_WAVES && !LOOP ? SCW : 1)))
 void step_c_kernel(const DevEnv* __restrict__ dp, StepIO io) {
   constexpr int RREG = (WB <= 8 && K <= 8) ? OBS_RING_REG : 0;
   constexpr bool HSTAT = true;
@@ -1902,7 +1905,8 @@ static hipError_t launch_step_k(const EnvConst& c, const DevEnv* d, const StepIO
     a = c.obs_ring_reg ? (dbg ? (KFn)step_a_kernel<K, true, true> : (KFn)step_a_kernel<K, false, true>)
                        : (dbg ? (KFn)step_a_kernel<K, true> : (KFn)step_a_kernel<K, false>);
     cc = (c.W <= 8 && c.obs_ring_reg) ? (dbg ? (KFn)step_c_kernel<K, true, 8> : (KFn)step_c_kernel<K, false, 8>)
-                                      : (dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>);
+       : c.sc_form == 4 ? (dbg ? (KFn)step_c_kernel<K, true, STEP_WAVES, false, 4> : (KFn)step_c_kernel<K, false, STEP_WAVES, false, 4>)
+                        : (dbg ? (KFn)step_c_kernel<K, true> : (KFn)step_c_kernel<K, false>);
   }
   const bool tab = c.sb_tab != 0;  // (capi.hip: small tables, or room at this occupancy)
   KFn b;

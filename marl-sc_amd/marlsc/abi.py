@@ -105,6 +105,7 @@ def lib() -> C.CDLL:
     L.msc_env_ea_memory.argtypes = [vp, P(C.c_int64), P(C.c_int64)]
     L.msc_env_dims.argtypes = [vp, P(C.c_int64), ip, ip, ip, ip, ip, ip, ip]
     L.msc_env_kernel_choice.argtypes = [vp, ip, C.c_int32]
+    L.msc_env_set_option.argtypes = [vp, C.c_int32, C.c_int32]
     L.msc_env_reset.argtypes = [vp, vp, vp, C.c_int32, vp, vp]
     L.msc_env_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, P(MscStepInfo), vp]
     L.msc_env_obs_flat.argtypes = [vp, vp, vp, vp]
@@ -160,7 +161,7 @@ def check(rc: int) -> None:
 
 
 EXPORTED_SYMBOLS = [
-    "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_kernel_choice", "msc_env_ea_memory", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_episode_ahead", "msc_env_set_timing", "msc_env_read_timing", "msc_env_read_timing_ea", "msc_env_work_counters", "msc_env_obs_flat",
+    "msc_env_create", "msc_env_destroy", "msc_env_dims", "msc_env_kernel_choice", "msc_env_set_option", "msc_env_ea_memory", "msc_env_reset", "msc_env_step", "msc_env_generate_demand", "msc_env_set_pipelining", "msc_env_set_chain_priority", "msc_env_set_episode_ahead", "msc_env_set_timing", "msc_env_read_timing", "msc_env_read_timing_ea", "msc_env_work_counters", "msc_env_obs_flat",
     "msc_env_read_state", "msc_env_state_bytes", "msc_env_save_state", "msc_env_load_state", "msc_env_check",
     "msc_env_set_episode_counters", "msc_gae", "msc_adv_normalize", "msc_gae_grouped", "msc_adv_normalize_grouped", "msc_gaussian_sample", "msc_mlp3_w3_layout", "msc_mlp3_relu_forward", "msc_mlp2_relu_forward",
     "msc_mlp3_relu_forward_sampled", "msc_mlp2_relu_forward_sampled",

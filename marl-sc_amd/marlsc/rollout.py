@@ -449,6 +449,13 @@ class RolloutCollector:
         # (the kernel clamps at logstd_floor), no clamp / broadcast launches per step
         self._ls = m.log_std_table() if hasattr(m, "log_std_table") and hasattr(m, "actor_mean") else None
         for ln in self._lanes:
+            if not getattr(ln, "form_set", False) and hasattr(ln.env, "set_option"):
+                # the observation kernel's spill-free form: with policy kernels between the steps it
+                # is faster than the form the env stepping uses beside the demand kernel (C3 MAPPO
+                # rollout 1.18 -> 1.14 ms per step, profiles/r06/ab_step_c_wpe.txt); results identical
+                if os.environ.get("MSC_ROLLOUT_STEP_C_FORM", "4") == "4":
+                    ln.env.set_option(ln.env.STEP_C_FORM, 4)
+                ln.form_set = True
             if os.environ.get("MSC_ROLLOUT_CHAIN_PRIO", "0") != "0" and not getattr(ln, "prio_set", False):
                 # A/B: step chain ahead of the next step's demand kernel (neutral: 1.234 vs 1.228 ms
                 # per step; the step kernels wait for CU space, not for issue slots)

@@ -185,6 +185,12 @@ class VecInventoryEnv:
         abi.check(abi.lib().msc_env_ea_memory(self._h, C.byref(b), C.byref(a)))
         return {"budget": b.value, "allocated": a.value, "slots": self.ea_slots}
 
+    STEP_C_FORM = 1  # include/marlsc.h MSC_OPT_STEP_C_FORM
+
+    def set_option(self, key: int, value: int) -> None:
+        """A kernel-form option of this handle (msc_env_set_option; results are identical)."""
+        abi.check(abi.lib().msc_env_set_option(self._h, int(key), int(value)))
+
     def kernel_choice(self) -> Dict[str, int]:
         """The kernels this handle runs (msc_env_kernel_choice), chosen at create time by shape."""
         keys = ("alloc", "alloc_sort", "fuse_a", "fuse_c", "group_tables_lds", "group_width", "ea_slots",

@@ -154,6 +154,18 @@ def test_bench_config_vs_oracle_across_episode_boundary():
     _lockstep(spec, 512, 110, check_every=10)
 
 
+@pytest.mark.parametrize("form", ["4", "5"])
+def test_step_c_forms_vs_oracle(monkeypatch, form):
+    # the observation kernel's two register forms (MSC_OPT_STEP_C_FORM / MSC_STEP_C_FORM: 5 waves per
+    # SIMD with spills, the env stepping default; 4, the rollout collector's), through the lane
+    # allocator and the 16-wave step_c, across an episode boundary
+    _set_alloc(monkeypatch, "lane")
+    monkeypatch.setenv("MSC_STEP_C_FORM", form)
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=20)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 256, 45, seed=13, check_every=5)
+
+
 @pytest.mark.parametrize("gen,ea", [(1, "0"), (2, "0"), (5, "0"), (7, "0"), (5, "1"), (7, "1")])
 def test_demand_generator_waves_vs_oracle(monkeypatch, gen, ea):
     # the Poisson demand kernel with 1 / 2 / 5 / 7 generator waves per 64 envs (MSC_DEMAND_GEN; every
