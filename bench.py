@@ -68,7 +68,18 @@ def issue_object(insts: float, seconds: float, clk_mhz=None, **extra) -> dict:
         o.update({"clock_mhz": clk_mhz, "peak_at_clock": round(pk / 1e9, 1), "frac_at_clock": round(ach / pk, 4)})
     return o
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
-DEMAND_KERNEL = "demand_unit_kernel"
+DEMAND_KERNEL = "demand_v3_kernel"  # the Poisson demand kernel of the headline handle (set in main)
+
+
+def demand_kernel_name(env) -> str:
+    """Base name of the demand kernel a handle runs (msc_env_kernel_choice's demand entry)."""
+    impl = env.kernel_choice().get("demand_impl", 0)
+    return {9: "demand_v3_kernel", 8: "demand_v2_kernel", 7: "demand_ab_kernel", 5: "demand_park4_kernel"}.get(
+        impl, "demand_unit_kernel")
+
+
+def is_demand_kernel(name: str) -> bool:
+    return name.startswith("demand_") or name in ("reset_kernel", "ea_materialize_kernel")
 STEP_KERNELS = ("step_a_kernel", "alloc_lane_kernel", "step_c_kernel")
 GAE_BYTES_PER_ELEM = 4 + 4 + 1 + 1 + 4 + 4  # reward, value, terminated, truncated in; advantage, target out (next value: truncated rows only)
 
@@ -301,8 +312,7 @@ def c2_line(args, rank: int):
         tr = json.loads(tj.read_text())
         key = f"{spec.W}x{spec.R}x{spec.K}x{E}"
         cs = tr.get("counters", {}).get(key, {})
-        names = tuple(n for n in cs if n not in (DEMAND_KERNEL, DEMAND_KERNEL + "_ea", "reset_kernel",
-                                                 "ea_materialize_kernel")) or ("step_a_kernel", "alloc_scan_kernel", "step_c_kernel")
+        names = tuple(n for n in cs if not is_demand_kernel(n)) or ("step_a_kernel", "alloc_scan_kernel", "step_c_kernel")
         cn = [cs.get(n, {}).get("SQ_INSTS_VALU") for n in names]
         tb = [tr.get(key, {}).get(n) for n in names]
         if all(x is not None for x in cn) and tm["step_ms"] > 0:
@@ -595,6 +605,8 @@ def main():
                           episode_ahead=16 if want_ea else None)
     if env.ea_slots and E > 8192:
         env.set_episode_ahead(False)
+    global DEMAND_KERNEL
+    DEMAND_KERNEL = demand_kernel_name(env)
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
     pool = [torch.rand((E, spec.W, spec.K), generator=g, device="cuda") * 2 - 1 for _ in range(8)]
     env.reset()
@@ -757,8 +769,7 @@ def main():
         if tj.exists():
             tr = json.loads(tj.read_text())
             # the phase kernels this workload ran (allocation: lane / group (+ order sort) / scan)
-            step_names = tuple(n for n in tr.get(key, {}) if n not in (DEMAND_KERNEL, DEMAND_KERNEL + "_ea", "reset_kernel",
-                                                                        "ea_materialize_kernel"))
+            step_names = tuple(n for n in tr.get(key, {}) if not is_demand_kernel(n))
             names = (step_names or STEP_KERNELS) if dom == "step_kernels" else (dom,)
             tb = [tr.get(key, {}).get(n) for n in names]
             traffic = sum(tb) if all(x is not None for x in tb) else None

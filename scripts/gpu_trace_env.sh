@@ -14,7 +14,7 @@ import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 def short(n):
-    for k in ("demand_v3", "demand_unit", "demand_v2", "alloc_lane", "alloc_scan", "step_a", "step_b", "step_c", "alloc_sort", "reset"):
+    for k in ("demand_v3", "demand_unit", "demand_v2", "alloc_lane", "alloc_scan", "step_a", "step_b", "step_c", "alloc_sort", "reset", "ea_materialize"):
         if k in n: return k
     return n[:30]
 big = [r for r in rows if int(r.get("Grid_Size", r.get("Grid_Size_X", "0")) or 0) >= 32768 * 4 or "alloc_lane" in r["Kernel_Name"]]

@@ -12,7 +12,7 @@ import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 def short(n):
-    for k in ("demand_unit", "alloc_lane", "step_a", "step_c", "mlp3_relu_kernel<8", "mlp3_relu_kernel<2", "mlp2_relu", "meanstd", "obs_filter", "gae4", "gauss", "Cijk", "elementwise", "reduce"):
+    for k in ("demand_v3", "demand_unit", "alloc_lane", "step_a", "step_c", "mlp3_relu_kernel<8", "mlp3_relu_kernel<2", "mlp2_relu", "meanstd", "obs_filter", "gae4", "gauss", "Cijk", "elementwise", "reduce"):
         if k in n: return k
     return n[:30]
 # last 400 kernels: print name, start (us rel), end, queue id

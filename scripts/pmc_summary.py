@@ -31,7 +31,7 @@ def base_name(full: str) -> str:
     if not m:
         return ""
     name = m.group(1)
-    if name == "demand_unit_kernel" and (m.group(2) or "").replace(" ", "").endswith(",true"):
+    if name.startswith("demand_") and (m.group(2) or "").replace(" ", "").endswith(",true"):
         name += "_ea"
     return name
 
