@@ -52,7 +52,12 @@ struct msc_env {
   // demand stream) or the envs' timesteps are out of sync after a masked reset.
   hipStream_t side = nullptr;
   hipEvent_t ev_dem[2] = {nullptr, nullptr}, ev_step[2] = {nullptr, nullptr}, ev_reset = nullptr;
-  int64_t tau = 0;                 // steps issued
+  // the stream each ev_dem was last recorded on (a wait from that same stream is already ordered),
+  // and whether the side stream has waited on the latest ev_reset (a reset is recorded once)
+  hipStream_t ev_dem_on[2] = {nullptr, nullptr};
+  bool side_saw_reset = false;
+  bool ev_elide = true;  // MSC_EV_ELIDE=0: every wait is issued (A/B)
+  int64_t tau = 0;                // steps issued
   int t_sync = -1;                 // common timestep of every env, -1 if unknown
   bool ready[2] = {false, false};  // order buffer b holds the demand of the next step using it
   bool pipeline = true;
@@ -825,17 +830,25 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   }
   if (hipStreamCreateWithFlags(&env->side, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(-2, "side stream creation failed"));
+  // the pipelining events only order work between two streams of this device: MSC_EV_SCOPE=device
+  // records them with a device-scope release, =nofence without the system-scope fence (A/B)
+  unsigned evf = hipEventDisableTiming;
+  if (const char* es = getenv("MSC_EV_SCOPE"))
+    evf |= strcmp(es, "device") == 0 ? hipEventReleaseToDevice : strcmp(es, "nofence") == 0 ? hipEventDisableSystemFence : 0u;
   for (int b = 0; b < 2; b++)
-    if (hipEventCreateWithFlags(&env->ev_dem[b], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&env->ev_step[b], hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&env->ev_dem[b], evf) != hipSuccess ||
+        hipEventCreateWithFlags(&env->ev_step[b], evf) != hipSuccess)
       return fail(set_err(-2, "event creation failed"));
-  if (hipEventCreateWithFlags(&env->ev_reset, hipEventDisableTiming) != hipSuccess)
+  if (hipEventCreateWithFlags(&env->ev_reset, evf) != hipSuccess)
     return fail(set_err(-2, "event creation failed"));
   for (int b = 0; b < 2; b++) {  // recorded once so that every later wait is well-defined
     (void)hipEventRecord(env->ev_dem[b], env->side);
+    env->ev_dem_on[b] = env->side;
     (void)hipEventRecord(env->ev_step[b], env->side);
   }
   (void)hipEventRecord(env->ev_reset, env->side);
+  env->side_saw_reset = true;
+  if (const char* el = getenv("MSC_EV_ELIDE")) env->ev_elide = strcmp(el, "0") != 0;
   if (env->ea_enabled) {
     // MSC_EA_PRIO=low|high: queue priority of the generation stream (A/B; default: normal)
     int ea_prio = 0, lo = 0, hi = 0;
@@ -941,6 +954,7 @@ int msc_env_reset(msc_env* env, const uint8_t* mask, const uint32_t* new_root_se
   env->t_sync = mask ? -1 : 0;
   HIP_TRY(launch_reset(env->c, env->dev, mask, new_root_seeds, flags, obs, st));
   HIP_TRY(hipEventRecord(env->ev_reset, st));
+  env->side_saw_reset = false;
   return 0;
 }
 
@@ -998,6 +1012,7 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
       env->cnt_dem_launch++;
       HIP_TRY(tmark(env, env->tev_dem, env->n_tdem++, 1, st));
       HIP_TRY(hipEventRecord(env->ev_dem[b], st));
+      env->ev_dem_on[b] = st;
     }
   }
   HIP_TRY(tmark(env, env->tev_step, env->n_tstep, 0, st));
@@ -1023,14 +1038,21 @@ int msc_env_step(msc_env* env, const float* actions, float* obs, float* rewards,
     // demand of step tau+1 into the other buffer, concurrently with this step kernel; that buffer
     // was last read by step tau-1, and the demand stream was last advanced by demand(tau)
     const int nb = b ^ 1;
+    // (a wait already ordered by the side stream itself is not issued: each costs a barrier packet
+    // the command processor retires between the demand launches, which bound a pipelined step)
     HIP_TRY(hipStreamWaitEvent(env->side, env->ev_step[nb], 0));
-    HIP_TRY(hipStreamWaitEvent(env->side, env->ev_dem[b], 0));
-    HIP_TRY(hipStreamWaitEvent(env->side, env->ev_reset, 0));
+    if (!env->ev_elide || env->ev_dem_on[b] != env->side)
+      HIP_TRY(hipStreamWaitEvent(env->side, env->ev_dem[b], 0));
+    if (!env->ev_elide || !env->side_saw_reset) {
+      HIP_TRY(hipStreamWaitEvent(env->side, env->ev_reset, 0));
+      env->side_saw_reset = true;
+    }
     HIP_TRY(tmark(env, env->tev_dem, env->n_tdem, 0, env->side));
     HIP_TRY(launch_demand(c, env->dev + nb, env->side));
     env->cnt_dem_launch++;
     HIP_TRY(tmark(env, env->tev_dem, env->n_tdem++, 1, env->side));
     HIP_TRY(hipEventRecord(env->ev_dem[nb], env->side));
+    env->ev_dem_on[nb] = env->side;
     env->ready[nb] = true;
   }
   env->t_sync = env->t_sync < 0 ? -1 : (env->t_sync + 1 >= c.T ? 0 : env->t_sync + 1);
@@ -1183,6 +1205,7 @@ int msc_env_generate_demand(msc_env* env, msc_stream_t stream) {
   HIP_TRY(launch_demand(env->c, env->dev + b, st));
   env->cnt_dem_launch++;
   HIP_TRY(hipEventRecord(env->ev_dem[b], st));
+  env->ev_dem_on[b] = st;
   env->ready[b] = true;
   return 0;
 }
@@ -1275,6 +1298,7 @@ int msc_env_load_state(msc_env* env, const void* buf) {
                       hipMemcpyHostToDevice));
     env->ready[b] = true;
     HIP_TRY(hipEventRecord(env->ev_dem[b], env->side));
+    env->ev_dem_on[b] = env->side;
   }
   env->t_sync = h.t_sync;
   return 0;
