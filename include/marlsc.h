@@ -179,14 +179,19 @@ int msc_env_dims(const msc_env* env, int64_t* n_envs, int32_t* n_agents, int32_t
  * runs, chosen at create time from its shape and the MSC_* knobs. Writes up to n of
  * {alloc (0 lane, 1 group, 2 scan), envs sorted by order count, phase A fused, phase C fused,
  *  group kernel cost tables in LDS, lane-group width, episode-ahead slots, demand (0 unit parser,
- *  5 park4, 7 split parser), equal sampler parameters (UNI)}; returns the count written. */
+ *  5 park4, 7 split parser, 8 f32-ring parser, 9 demand_v3), equal sampler parameters (UNI)}; returns the
+ *  count written. */
 int msc_env_kernel_choice(const msc_env* env, int32_t* out, int32_t n);
 
 /* Kernel-form options of a handle that change no result (diagnostic / tuning; no reference
  * counterpart). MSC_OPT_STEP_C_FORM: the waves per SIMD the observation kernel is compiled for, 5
  * (default: beside the pipelined demand kernel) or 4 (no register spills; the rollout collector's
- * choice, with policy kernels between steps). Returns 0, or < 0 for an unknown key / value. */
+ * choice, with policy kernels between steps). MSC_OPT_ALLOC_PRIO_SPLIT: the share, in 16ths of its
+ * busiest env's orders, that each one-env-per-lane allocation wave runs above the pipelined demand
+ * kernel's parser (s_setprio 3) before it drops below it (1 .. 16; default 12; 16: the whole kernel,
+ * the rollout collector's choice). Returns 0, or < 0 for an unknown key / value. */
 #define MSC_OPT_STEP_C_FORM 1
+#define MSC_OPT_ALLOC_PRIO_SPLIT 2
 int msc_env_set_option(msc_env* env, int32_t key, int32_t value);
 
 #define MSC_RESET_EVAL_RESTART 1  /* reset(seed=...) of a construction-seeded eval env: counter -> 0 */

@@ -37,6 +37,9 @@ hipError_t launch_alloc_lane_k(const EnvConst& c, const DevEnv* d, const StepIO&
 #ifndef MSC_AL_PRIO
 #define MSC_AL_PRIO 3  // s_setprio: the step chain is the critical path next to the demand waves
 #endif
+#ifndef MSC_AL_PRIO2
+#define MSC_AL_PRIO2 1  // the priority after c.al_psplit 16ths of the orders: below the demand parser (2)
+#endif
 
 // LDS layout of one block (64 envs); word offsets
 struct AlLds {
@@ -297,7 +300,12 @@ __global__ __launch_bounds__(64) void alloc_lane_kernel(const DevEnv* __restrict
   publish();
   fetch(1);
 
+  // the first c.al_psplit 16ths of the orders above the next step's demand parser, the rest below it
+  // (msc_env_set_option MSC_OPT_ALLOC_PRIO_SPLIT; 16: all of them)
+  const int aps = __builtin_amdgcn_readfirstlane(c.chain_prio ? 16 : c.al_psplit);
+  const int psplit = MSC_AL_PRIO > 0 && aps < 16 ? (wmax * aps) >> 4 : -1;
   for (int oi = 0; oi <= wmax; oi++) {
+    if (oi == psplit) __builtin_amdgcn_s_setprio(MSC_AL_PRIO2);
     const int jw = oi % AL_CH;
     if (jw == 0 && oi > 0) {  // wave-uniform: window oi / AL_CH is due, start the one after
       publish();

@@ -513,6 +513,12 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
     c.sc_tab = 1;
     c.sc_form = 5;
     if (const char* sf = getenv("MSC_STEP_C_FORM")) c.sc_form = atoi(sf) == 4 ? 4 : 5;
+    // alloc_lane's waves run above the parser of the next step's demand kernel for the first 12/16
+    // of their orders, then below it: the pipelined C3 step is demand-bound with the allocation at
+    // full priority (0.755 ms demand beside 0.64 ms of step kernels) and chain-bound below it (0.61
+    // beside 0.86); 12/16 balances them (341 -> 349 M agent-steps/s, profiles/r06/ab_alloc_prio.txt)
+    c.al_psplit = 12;
+    if (const char* ps = getenv("MSC_AL_PRIO_SPLIT")) c.al_psplit = atoi(ps) >= 1 && atoi(ps) <= 16 ? atoi(ps) : 12;
     if (const char* st = getenv("MSC_SC_TAB")) c.sc_tab = atoi(st) != 0 ? 1 : 0;
     c.sb_gw = 0;
     if (const char* g = getenv("MSC_SB_GW")) {
@@ -1114,6 +1120,16 @@ int msc_env_set_option(msc_env* env, int32_t key, int32_t value) {
   if (key == MSC_OPT_STEP_C_FORM) {
     if (value != 4 && value != 5) return set_err(-1, "MSC_OPT_STEP_C_FORM must be 4 or 5");
     env->c.sc_form = value;  // (host-side launch choice: the device descriptor does not carry it)
+    return 0;
+  }
+  if (key == MSC_OPT_ALLOC_PRIO_SPLIT) {
+    if (value < 1 || value > 16) return set_err(-1, "MSC_OPT_ALLOC_PRIO_SPLIT must be in 1 .. 16");
+    if (env->c.al_psplit == value) return 0;
+    env->c.al_psplit = value;
+    HIP_TRY(hipSetDevice(env->device));
+    HIP_TRY(hipDeviceSynchronize());  // no launch in flight reads the descriptors being patched
+    for (int b = 0; b < 2; b++)
+      HIP_TRY(hipMemcpy(&env->dev[b].c.al_psplit, &value, sizeof value, hipMemcpyHostToDevice));
     return 0;
   }
   return set_err(-1, "unknown option %d", key);

@@ -53,6 +53,7 @@ struct EnvConst {
   int32_t sb_gw;        // step_b lane-group width forced wider than the warehouse count (MSC_SB_GW; 0: by W)
   int32_t sc_tab;       // alloc_scan_kernel stages the {of, ov} table in LDS (when it fits: TAB form)
   int32_t sc_form;      // step_c_kernel's 16-wave form: compiled for 5 (env stepping) or 4 (rollout) waves per SIMD
+  int32_t al_psplit;    // alloc_lane: 16ths of the wave's busiest env's orders run at s_setprio 3, the rest at 1
   uint32_t flags;
   int64_t E;
   int64_t ea_cap;       // episode-ahead demand: order records per (slot, env) episode

@@ -455,6 +455,10 @@ class RolloutCollector:
                 # rollout 1.18 -> 1.14 ms per step, profiles/r06/ab_step_c_wpe.txt); results identical
                 if os.environ.get("MSC_ROLLOUT_STEP_C_FORM", "4") == "4":
                     ln.env.set_option(ln.env.STEP_C_FORM, 4)
+                # the allocation at full priority for its whole run: here the step chain, not the
+                # demand kernel beside it, bounds a step (the env stepping's 12/16 split costs the C3
+                # MAPPO rollout 1.14 -> 1.18 ms per step, profiles/r06/ab_alloc_prio.txt)
+                ln.env.set_option(ln.env.ALLOC_PRIO_SPLIT, int(os.environ.get("MSC_ROLLOUT_AL_PRIO_SPLIT", "16")))
                 ln.form_set = True
             if os.environ.get("MSC_ROLLOUT_CHAIN_PRIO", "0") != "0" and not getattr(ln, "prio_set", False):
                 # A/B: step chain ahead of the next step's demand kernel (neutral: 1.234 vs 1.228 ms

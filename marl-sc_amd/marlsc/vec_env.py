@@ -186,6 +186,7 @@ class VecInventoryEnv:
         return {"budget": b.value, "allocated": a.value, "slots": self.ea_slots}
 
     STEP_C_FORM = 1  # include/marlsc.h MSC_OPT_STEP_C_FORM
+    ALLOC_PRIO_SPLIT = 2  # include/marlsc.h MSC_OPT_ALLOC_PRIO_SPLIT
 
     def set_option(self, key: int, value: int) -> None:
         """A kernel-form option of this handle (msc_env_set_option; results are identical)."""

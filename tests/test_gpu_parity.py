@@ -166,6 +166,44 @@ def test_step_c_forms_vs_oracle(monkeypatch, form):
     _lockstep(spec, 256, 45, seed=13, check_every=5)
 
 
+@pytest.mark.parametrize("split", ["1", "16"])
+def test_alloc_prio_split_vs_oracle(monkeypatch, split):
+    # alloc_lane's priority drop after split/16 of its orders (MSC_OPT_ALLOC_PRIO_SPLIT; default 12,
+    # run by every other lane test): scheduling only, results identical
+    _set_alloc(monkeypatch, "lane")
+    monkeypatch.setenv("MSC_AL_PRIO_SPLIT", split)
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=20)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    _lockstep(spec, 256, 25, seed=17, check_every=5)
+
+
+def test_set_option_mid_run_matches_default(monkeypatch):
+    # msc_env_set_option between steps (the rollout collector's step_c form 4 and whole-kernel
+    # allocation priority) changes no result: two handles on the same seeds, one switched after 7
+    # steps, stay bit-identical across an episode boundary; bad keys / values raise
+    _set_alloc(monkeypatch, "lane")
+    cfg = make_synthetic_env_config(8, 64, 5, episode_length=12)
+    spec = EnvSpec.from_config(cfg, {"include_warehouse_id": True})
+    a, b = _vec(spec, 192, base_seed=5), _vec(spec, 192, base_seed=5)
+    np.testing.assert_array_equal(_np(a.reset()), _np(b.reset()))
+    rng = np.random.default_rng(3)
+    for t in range(20):
+        if t == 7:
+            b.set_option(b.STEP_C_FORM, 4)
+            b.set_option(b.ALLOC_PRIO_SPLIT, 16)
+        if t == 13:
+            b.set_option(b.ALLOC_PRIO_SPLIT, 3)
+        act = torch.from_numpy(rng.uniform(-1, 1, size=(192, spec.W, spec.K)).astype(np.float32)).cuda()
+        oa, _, ta, _ = a.step(act, want_f64=True)
+        ob, _, tb, _ = b.step(act, want_f64=True)
+        np.testing.assert_array_equal(_np(oa), _np(ob), err_msg=f"obs t={t}")
+        np.testing.assert_array_equal(_np(a.rewards_f64), _np(b.rewards_f64), err_msg=f"rewards t={t}")
+        np.testing.assert_array_equal(_np(ta), _np(tb))
+    for key, val in ((b.ALLOC_PRIO_SPLIT, 0), (b.ALLOC_PRIO_SPLIT, 17), (b.STEP_C_FORM, 3), (99, 1)):
+        with pytest.raises(Exception):
+            b.set_option(key, val)
+
+
 @pytest.mark.parametrize("gen,ea", [(1, "0"), (2, "0"), (5, "0"), (7, "0"), (5, "1"), (7, "1")])
 def test_demand_generator_waves_vs_oracle(monkeypatch, gen, ea):
     # the Poisson demand kernel with 1 / 2 / 5 / 7 generator waves per 64 envs (MSC_DEMAND_GEN; every
