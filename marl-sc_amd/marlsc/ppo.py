@@ -50,6 +50,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from . import dist as mdist
 from .rollout import MLP, RolloutCollector, RolloutConfig, fused_actor_sample, mlp_forward, split_global_mlp
 
 LOG2PI = math.log(2 * math.pi)
@@ -509,8 +510,11 @@ class PPOTrainer:
         # rollout length: RLlib's train batch counts env steps over every runner of every rank
         self.T = int(rollout_len or max(1, math.ceil(cfg.batch_size / (E * self.world))))
         self.device = torch.device("cuda", device)
+        # weak partition: rank g steps global env ids [g E, (g + 1) E); ranks sharing a device split
+        # the episode-ahead memory budget
         self.env = VecInventoryEnv(None, E, spec=self.spec, device=device, base_seed=self.train_seed,
-                                   env_index_offset=self.rank * E)
+                                   env_index_offset=mdist.shard(E, "weak", self.rank, self.world)[1],
+                                   ea_mem_fraction=mdist.ea_mem_fraction())
         rc = cfg.rollout_config()
         torch.manual_seed(self.train_seed)
         W, L = self.env.W, self.env.local_obs_dim
