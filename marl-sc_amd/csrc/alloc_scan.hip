@@ -378,7 +378,7 @@ __device__ __forceinline__ void fc_obs_lane(const EnvConst& c, const ScFcLds* Lf
 // observations, the in-kernel reset at truncation; one slot per lane, rings of <= SC_FC_RING slots).
 // FA (with FC): phase A fused too (step_a_kernel: action rescale, orders into the ring, arrivals,
 // inbound cost) for fixed lead times and Poisson demand (no per-env RNG work in phase A)
-template <int K, int GW, bool TAB, bool FC = false, bool FA = false>
+template <int K, int GW, bool TAB, bool FC = false, bool FA = false, bool ND = false>
 __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(GW > 8 ? 3 : MSC_SC_WPE))) void alloc_scan_kernel(
     const DevEnv* __restrict__ dp, StepIO io) {
   constexpr int SPW = 64 / GW;        // SKU groups per wave
@@ -404,7 +404,9 @@ __global__ __launch_bounds__(64 * SC_WAVES) __attribute__((amdgpu_waves_per_eu(G
     lvj[j] = skj[j] < K && w < W;
   }
   const msc_step_info info = io.info;
-  const bool dbg = io.has_info != 0;
+  // ND: an instantiation without the step-info stores (io.has_info == 0): their pointers, flags and
+  // branches out of the registers of the order loop
+  const bool dbg = !ND && io.has_info != 0;
   if (MSC_SC_PRIO > 0) __builtin_amdgcn_s_setprio(MSC_SC_PRIO);
 
   extern __shared__ __attribute__((aligned(16))) char sc_lds[];
@@ -1072,13 +1074,21 @@ bool alloc_scan_fuse_supported(int W, int K, int RING) { return W <= 8 && K <= 6
 // above 4 SKUs)
 bool alloc_scan_supported(int W, int K) { return W <= 16 && K <= 6; }
 
+#ifndef MSC_SC_ND
+#define MSC_SC_ND 1  // the fused scan step without step info runs its no-info instantiation
+#endif
 template <int K>
 static hipError_t launch_scan_k(const EnvConst& c, const DevEnv* d, const StepIO& io, hipStream_t st) {
   using KFn = void (*)(const DevEnv*, StepIO);
   const int GW = sc_gw(c.W);
   const bool t = alloc_scan_tab(c, GW);
   KFn f;
-  if (c.fuse_c && c.fuse_a) {
+  if (c.fuse_c && c.fuse_a && MSC_SC_ND && !io.has_info) {
+    f = GW == 2 ? (t ? (KFn)alloc_scan_kernel<K, 2, true, true, true, true> : (KFn)alloc_scan_kernel<K, 2, false, true, true, true>)
+      : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true, true, true, true> : (KFn)alloc_scan_kernel<K, 4, false, true, true, true>)
+                : (t ? (KFn)alloc_scan_kernel<K, 8, true, true, true, true> : (KFn)alloc_scan_kernel<K, 8, false, true, true, true>);
+    if (GW > 8) return hipErrorInvalidValue;
+  } else if (c.fuse_c && c.fuse_a) {
     f = GW == 2 ? (t ? (KFn)alloc_scan_kernel<K, 2, true, true, true> : (KFn)alloc_scan_kernel<K, 2, false, true, true>)
       : GW == 4 ? (t ? (KFn)alloc_scan_kernel<K, 4, true, true, true> : (KFn)alloc_scan_kernel<K, 4, false, true, true>)
                 : (t ? (KFn)alloc_scan_kernel<K, 8, true, true, true> : (KFn)alloc_scan_kernel<K, 8, false, true, true>);
