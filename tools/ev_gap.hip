@@ -41,6 +41,10 @@ int main(int argc, char** argv) {
   CK(hipStreamCreateWithFlags(&main_s, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
   const int blocks = 512;
+  // stream memory operations instead of events (patterns 6, 7): one 32-bit counter per direction
+  unsigned *cnt_dem = nullptr, *cnt_step = nullptr;
+  CK(hipExtMallocWithFlags((void**)&cnt_dem, 8, hipMallocSignalMemory));
+  CK(hipExtMallocWithFlags((void**)&cnt_step, 8, hipMallocSignalMemory));
   for (int f = 0; f < 3; f++) {
     hipEvent_t ev_dem[2], ev_step[2];
     for (int b = 0; b < 2; b++) {
@@ -53,13 +57,15 @@ int main(int argc, char** argv) {
     CK(hipEventCreateWithFlags(&ev_pre, flags_list[f]));
     CK(hipEventRecord(ev_pre, main_s));
     CK(hipDeviceSynchronize());
-    for (int pat = 0; pat < 6; pat++) {
+    for (int pat = 0; pat < 8; pat++) {
       // 0: demand kernels back to back on one stream
       // 1: the same with an event record after each
       // 2: the pipelined pattern (side: wait step(t-1), demand(t+1), record; main: wait demand(t), 3 step kernels, record)
       // 3: pattern 2 with the demand on the main stream's side swapped (step chain longer than demand)
       // 4: pattern 2 without the side stream's wait (main waits on the demand only)
       // 5: demand kernels, each after a wait on an event completed long before
+      // 6: pattern 2 with hipStreamWriteValue32 / hipStreamWaitValue32 (>=) on counters instead of events
+      // 7: pattern 6 without the side stream's wait
       for (int rep = 0; rep < 2; rep++) {
         CK(hipDeviceSynchronize());
         const double t0 = now_ms();
@@ -70,6 +76,21 @@ int main(int argc, char** argv) {
           } else if (pat == 1) {
             spin<<<blocks, 64, 0, side>>>(dem, out);
             CK(hipEventRecord(ev_dem[b], side));
+          } else if (pat >= 6) {
+            if (t == 0) {
+              CK(hipMemsetAsync(cnt_dem, 0, 8, side));
+              CK(hipMemsetAsync(cnt_step, 0, 8, side));
+              CK(hipStreamSynchronize(side));
+            }
+            // demand t is signalled as count t + 1 (demand 0 is "done" before the loop)
+            CK(hipStreamWaitValue32(main_s, cnt_dem, (unsigned)t, hipStreamWaitValueGte, 0xffffffffu));
+            spin<<<blocks, 64, 0, main_s>>>(stp / 30, out + 1024);
+            spin<<<blocks, 64, 0, main_s>>>(stp * 20 / 30, out + 2048);
+            spin<<<blocks, 64, 0, main_s>>>(stp * 9 / 30, out + 3072);
+            CK(hipStreamWriteValue32(main_s, cnt_step, (unsigned)t + 1, 0));
+            if (pat == 6 && t >= 1) CK(hipStreamWaitValue32(side, cnt_step, (unsigned)t, hipStreamWaitValueGte, 0xffffffffu));
+            spin<<<blocks, 64, 0, side>>>(dem, out);
+            CK(hipStreamWriteValue32(side, cnt_dem, (unsigned)t + 1, 0));
           } else if (pat == 5) {
             CK(hipStreamWaitEvent(side, ev_pre, 0));
             spin<<<blocks, 64, 0, side>>>(dem, out);
@@ -100,5 +121,7 @@ int main(int argc, char** argv) {
     }
   }
   CK(hipFree(out));
+  CK(hipFree(cnt_dem));
+  CK(hipFree(cnt_step));
   return 0;
 }
