@@ -65,7 +65,10 @@ __device__ __forceinline__ void sample_row(const MlpSample& sm, int64_t j, int K
 // MFMAs). Each lane accumulates its half of the hidden units into VKO f32 sums with the weights read
 // from LDS (all lanes of a half read the same 32 bytes: broadcast), and the two halves are added
 // with one lane exchange. The packed w3 is then [NT2 * 16][2][8] floats (zero past KO).
-template <int NT1, int NT2, int P, int WPE, int VKO>
+// IL (VKO > 0, P < NT2): the VALU output layer of pass p - 1 interleaved into the layer-2 MFMA stream
+// of pass p (IPS units per k step), so its VALU work issues while the MFMAs execute instead of after
+// them; only the last pass's output layer runs alone. Same accumulation order as IL = false.
+template <int NT1, int NT2, int P, int WPE, int VKO, bool IL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void mlp3_relu_kernel(
     const float* __restrict__ x, int64_t n, int L, int KS1, const float4* __restrict__ w1p, const float* __restrict__ b1,
     const float4* __restrict__ w2p, const float* __restrict__ b2, const float4* __restrict__ w3p,
@@ -166,6 +169,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       a3[r] = row < KO ? b3[row] : 0.0f;
     }
   }
+  // one unit of the VALU output layer: hidden unit (tile q of pass pp, register r) into the outputs
+  auto l3_unit = [&](const mlp_f32x16 (&src)[P], int pp, int q, int r) {
+    if constexpr (VKO > 0) {
+      const float hv = fmaxf(src[q][r], 0.0f);
+      const int sidx = ((pp * P + q) * 16 + r) * 2 + h;
+      const float4 wa = w3s[sidx * 2];
+      const float wv[8] = {wa.x, wa.y, wa.z, wa.w, 0.f, 0.f, 0.f, 0.f};
+      float wh[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (VKO > 4) {
+        const float4 wb = w3s[sidx * 2 + 1];
+        wh[0] = wb.x, wh[1] = wb.y, wh[2] = wb.z, wh[3] = wb.w;
+      }
+#pragma unroll
+      for (int a = 0; a < VKO; a++) o3[a] = fmaf(a < 4 ? wv[a] : wh[a - 4], hv, o3[a]);
+    }
+  };
+  constexpr bool ILV = IL && VKO > 0 && P < NT2;
+  constexpr int IPS = (P * 16 + S4 - 1) / S4;  // interleaved output-layer units per k step
+  mlp_f32x16 a2p[ILV ? P : 1];                 // the previous pass's layer-2 sums (ILV)
   float4 w[2][P];  // [step parity][tile]: the fragments of step s4 and s4 + 1
 #pragma unroll
   for (int q = 0; q < P; q++) w[0][q] = w2p[((int64_t)q * S4) * 64 + lane];
@@ -204,24 +226,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
           a2[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv, bv, a2[q], 0, 0, 0);
         }
       }
+      if constexpr (ILV) {  // the previous pass's output layer, IPS units behind these MFMAs
+        if (p > 0) {
+#pragma unroll
+          for (int i = 0; i < IPS; i++) {
+            const int u = s4 * IPS + i;
+            if (u < P * 16) l3_unit(a2p, p - 1, u / 16, u % 16);
+          }
+        }
+      }
     }
     if constexpr (VKO > 0) {  // layer 3 on the VALU: o[a] += W3[a][hidden] relu(h2) over this lane's half
+      if constexpr (ILV) {
+        if (p + 1 < NT2 / P) {  // (interleaved into the next pass)
+#pragma unroll
+          for (int q = 0; q < P; q++) a2p[q] = a2[q];
+          continue;
+        }
+      }
 #pragma unroll
       for (int q = 0; q < P; q++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const float hv = fmaxf(a2[q][r], 0.0f);
-          const int sidx = ((p * P + q) * 16 + r) * 2 + h;
-          const float4 wa = w3s[sidx * 2];
-          const float wv[8] = {wa.x, wa.y, wa.z, wa.w, 0.f, 0.f, 0.f, 0.f};
-          float wh[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (VKO > 4) {
-            const float4 wb = w3s[sidx * 2 + 1];
-            wh[0] = wb.x, wh[1] = wb.y, wh[2] = wb.z, wh[3] = wb.w;
-          }
-#pragma unroll
-          for (int a = 0; a < VKO; a++) o3[a] = fmaf(a < 4 ? wv[a] : wh[a - 4], hv, o3[a]);
-        }
+        for (int r = 0; r < 16; r++) l3_unit(a2, p, q, r);
       continue;
     }
     // layer 3 on this pass's slice: the fragments of tile q + 1 are in flight during tile q
@@ -407,14 +433,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   }
 }
 
-// layer-2 output tiles per pass at 256 hidden units: 8 (all of H2 at once, 1 wave per SIMD, default:
-// 1.547 vs 1.610 ms per rollout step) or 4 (<= 256 VGPRs, 2 waves per SIMD; MSC_MLP_P8=4, A/B)
+// layer-2 output tiles per pass at 256 hidden units, 1 wave per SIMD: 41 (default) = passes of 4
+// tiles with the VALU output layer of each pass interleaved into the next pass's MFMAs (IL; C3 MAPPO
+// rollout 1.139 -> 1.093 ms per step beside the demand kernel, profiles/r06/ab_mlp_il.txt), 21 = the
+// same with passes of 2, 8 = all of H2 in one pass and the output layer after it (rounds 2-5);
+// 4 / 2 = passes of 4 / 2 without interleaving at 2 waves per SIMD (<= 256 VGPRs, spills; A/B).
+// MSC_MLP_P8, read at each launch (a test compares the forms)
 static int mlp_p8() {
-  static const int v = [] {
-    const char* e = getenv("MSC_MLP_P8");
-    return (e && (atoi(e) == 4 || atoi(e) == 2)) ? atoi(e) : 8;
-  }();
-  return v;
+  const char* e = getenv("MSC_MLP_P8");
+  const int v = e ? atoi(e) : 41;
+  return (v == 8 || v == 4 || v == 2 || v == 41 || v == 21) ? v : 41;
 }
 // wave priority 3 (MSC_MLP_PRIO=0: default priority, A/B)
 static int mlp_prio() {
@@ -448,9 +476,10 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
   const float4* w1 = reinterpret_cast<const float4*>(w1p);
   const float4* w2 = reinterpret_cast<const float4*>(w2p);
   const float4* w3 = reinterpret_cast<const float4*>(w3p);
-#define MSC_MLP_LAUNCH(NT1, NT2, P, WPE, VKO)                                                                          \
-  hipLaunchKernelGGL((mlp3_relu_kernel<NT1, NT2, P, WPE, VKO>), grid, block, 0, st, x, n, L, KS1, w1, b1, w2, b2, w3, \
-                     b3, KO, out, pre1, grp, mlp_prio(), sm)
+#define MSC_MLP_LAUNCH_IL(NT1, NT2, P, WPE, VKO, IL)                                                                   \
+  hipLaunchKernelGGL((mlp3_relu_kernel<NT1, NT2, P, WPE, VKO, IL>), grid, block, 0, st, x, n, L, KS1, w1, b1, w2, b2,   \
+                     w3, b3, KO, out, pre1, grp, mlp_prio(), sm)
+#define MSC_MLP_LAUNCH(NT1, NT2, P, WPE, VKO) MSC_MLP_LAUNCH_IL(NT1, NT2, P, WPE, VKO, false)
   // the output layer on the VALU for KO <= 8 (VKO = 1, 2, 4, 5 or 8: the next supported count >= KO)
   const int vko = mlp3_valu_outputs(KO);
 #define MSC_MLP_VKO(NT1, NT2, P, WPE)                                 \
@@ -462,10 +491,21 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
     case 8: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 8); break;               \
     default: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 0); break;              \
   }
+#define MSC_MLP_VKO_IL(NT1, NT2, P, WPE)                                 \
+  switch (vko) {                                                         \
+    case 1: MSC_MLP_LAUNCH_IL(NT1, NT2, P, WPE, 1, true); break;         \
+    case 2: MSC_MLP_LAUNCH_IL(NT1, NT2, P, WPE, 2, true); break;         \
+    case 4: MSC_MLP_LAUNCH_IL(NT1, NT2, P, WPE, 4, true); break;         \
+    case 5: MSC_MLP_LAUNCH_IL(NT1, NT2, P, WPE, 5, true); break;         \
+    case 8: MSC_MLP_LAUNCH_IL(NT1, NT2, P, WPE, 8, true); break;         \
+    default: MSC_MLP_LAUNCH(NT1, NT2, P, WPE, 0); break;                 \
+  }
   // H1 held whole in registers, H2 in passes of P tiles; (NT1, P) sets the register budget
   // (16 NT1 + 24 P + ~48 per lane) and with it the waves per SIMD
   if (H1 == 256 && H2 == 256) {
-    if (mlp_p8() == 8) MSC_MLP_VKO(8, 8, 8, 1)
+    if (mlp_p8() == 41) MSC_MLP_VKO_IL(8, 8, 4, 1)
+    else if (mlp_p8() == 21) MSC_MLP_VKO_IL(8, 8, 2, 1)
+    else if (mlp_p8() == 8) MSC_MLP_VKO(8, 8, 8, 1)
     else if (mlp_p8() == 4) MSC_MLP_VKO(8, 8, 4, 2)
     else MSC_MLP_VKO(8, 8, 2, 2)
   } else if (H1 == 128 && H2 == 128) {
@@ -502,6 +542,8 @@ hipError_t launch_mlp3_relu(const float* x, int64_t n, int L, int H1, int H2, in
     return hipErrorInvalidValue;
   }
 #undef MSC_MLP_VKO
+#undef MSC_MLP_VKO_IL
+#undef MSC_MLP_LAUNCH_IL
 #undef MSC_MLP_LAUNCH
   return hipGetLastError();
 }

@@ -290,6 +290,33 @@ def test_fused_actor_sampling_equals_mlp_then_gaussian_kernel(L, hidden, KO, P, 
         assert torch.equal(got[0], a_ref) and torch.equal(got[1], lp_ref) and torch.equal(got[2], c_ref)
 
 
+@pytest.mark.parametrize("form", ["8", "21", "4"])
+def test_mlp3_pass_forms_bit_identical(monkeypatch, form):
+    # msc_mlp3_relu_forward's layer-2 pass forms at 256 x 256 (MSC_MLP_P8): the default 41 (passes of
+    # 4 tiles, output layer interleaved into the next pass) against 8 (one pass), 21 and 4 -- the same
+    # accumulation order, so means and the fused sampling outputs are bit-identical
+    from marlsc.mlp import mlp3_forward
+    from marlsc.rollout import MLP
+    torch.manual_seed(5)
+    mods = list(MLP(34, 5, {"hidden_sizes": [256, 256]}).cuda())
+    g = torch.Generator(device="cuda").manual_seed(3)
+    n = 4099  # ragged last tile
+    x = torch.randn(n, 34, device="cuda", generator=g)
+    eps = torch.randn(n, 5, device="cuda", generator=g)
+    ls = (torch.randn(1, 5, device="cuda", generator=g) - 1.0).contiguous()
+    outs = []
+    with torch.no_grad():
+        for f in ("41", form):
+            monkeypatch.setenv("MSC_MLP_P8", f)
+            m = torch.empty(n, 5, device="cuda")
+            a, lp, c = torch.empty(n, 5, device="cuda"), torch.empty(n, device="cuda"), torch.empty(n, 5, device="cuda")
+            mlp3_forward(mods, x, m, sample=(ls, -2.0, eps, a, lp, c))
+            torch.cuda.synchronize()
+            outs.append((m, a, lp, c))
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
 def test_rollout_with_fused_sampling_equals_the_two_launch_path(monkeypatch):
     # the collector's fused actor + sampling launch against its mean -> msc_gaussian_sample path on
     # the same env seeds and noise: every buffer identical
