@@ -388,16 +388,26 @@ class RolloutCollector:
         with torch.cuda.stream(ln.critic_stream):
             self._values_into(t, sl, obs, full)
 
+    def _noise_chunk(self, ln: _Lane) -> int:
+        per_step = max(1, self.actions[0, ln.e0:ln.e1].numel() * 4)
+        if os.environ.get("MSC_NOISE_CHUNK"):
+            return max(1, int(os.environ["MSC_NOISE_CHUNK"]))
+        return max(NOISE_CHUNK, min(self.T, (1 << 30) // per_step))
+
     def _step(self, ln: _Lane, t: int) -> None:
         env, m, sl = ln.env, self.module, slice(ln.e0, ln.e1)
         obs = self._obs_all[t, sl]
         full = self._full(ln, obs)
         if self._critic_side:
             self._critic_on_side(ln, t, sl, obs, full)
-        # standard-normal noise for NOISE_CHUNK steps of the lane at once (one launch instead of one
-        # per step), keyed by global env id
-        if t % NOISE_CHUNK == 0:
-            n = min(NOISE_CHUNK, self.T - t)
+        # standard-normal noise for `chunk` steps of the lane at once (one launch instead of one per
+        # step), keyed by global env id. The whole rollout's noise when it fits 1 GiB: a noise launch
+        # between step_c and the actor lets the next demand kernel reach the CUs before the actor,
+        # whose one 384-VGPR wave per SIMD then no longer fits beside the demand waves (the actor of
+        # that step 378 -> 906 us, profiles/r06/trace_roll_c3_r06il.txt)
+        chunk = self._noise_chunk(ln)
+        if t % chunk == 0:
+            n = min(chunk, self.T - t)
             if _TORCH_NOISE:  # A/B only: torch's generator (not shard-invariant)
                 if not hasattr(self, "_gen"):
                     self._gen = torch.Generator(device=obs.device).manual_seed(self._noise_seed & 0x7FFFFFFF)
@@ -405,7 +415,7 @@ class RolloutCollector:
             else:
                 ln.noise = keyed_normal((n,) + tuple(self.actions[t, sl].shape), ln.env.env_index_offset,
                                         self._noise_seed, self.noise_step + t)
-        eps = ln.noise[t % NOISE_CHUNK]
+        eps = ln.noise[t % chunk]
         a = None
         if self._ls is not None and hasattr(m, "actor_sample"):
             # actor forward + sampling + log-density + the env's clip in one kernel launch
