@@ -836,11 +836,15 @@ int msc_env_create(const msc_env_desc* d, int device, int64_t n_envs, uint32_t b
   }
   if (hipStreamCreateWithFlags(&env->side, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(-2, "side stream creation failed"));
-  // the pipelining events only order work between two streams of this device: MSC_EV_SCOPE=device
-  // records them with a device-scope release, =nofence without the system-scope fence (A/B)
-  unsigned evf = hipEventDisableTiming;
+  // the pipelining events only order work between two streams of this device (no host waits on
+  // them), so their records skip the system-scope fence: ~2 us less per record (tools/ev_gap.hip),
+  // C2 224 -> 227 M, C3 +0.3 % (profiles/r06/ab_ev_nofence.txt). MSC_EV_SCOPE=system restores it,
+  // =device records them with a device-scope release (A/B)
+  unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
   if (const char* es = getenv("MSC_EV_SCOPE"))
-    evf |= strcmp(es, "device") == 0 ? hipEventReleaseToDevice : strcmp(es, "nofence") == 0 ? hipEventDisableSystemFence : 0u;
+    evf = hipEventDisableTiming | (strcmp(es, "device") == 0   ? hipEventReleaseToDevice
+                                   : strcmp(es, "system") == 0 ? 0u
+                                                               : hipEventDisableSystemFence);
   for (int b = 0; b < 2; b++)
     if (hipEventCreateWithFlags(&env->ev_dem[b], evf) != hipSuccess ||
         hipEventCreateWithFlags(&env->ev_step[b], evf) != hipSuccess)
